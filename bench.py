@@ -1,0 +1,265 @@
+#!/usr/bin/env python3
+"""Headline benchmark: device-resident rs_vand encode + decode on MI355X.
+
+Metric (BASELINE.json): "device-resident encode+decode GiB/s, k=10 m=4,
+4 MiB objects, 1/2/4/8 GPU".  Workload = BASELINE configs[1] + configs[2]:
+a batch of 256 objects x 4 MiB per GPU (PCG64 seed 20261015 bytes), k=10,
+m=4, and for decode 4 random fragment erasures per object (same seed).
+
+One step = encode the batch (objects -> 4 parity fragments with headers,
+ecamd_encode_batch) + decode the batch (first 10 of the surviving fragments
+-> objects, ecamd_decode_batch).  Inputs are resident in HBM before timing.
+value = (bytes encoded + bytes decoded, all ranks) / step time, in GiB/s
+(2^30, user object bytes, like pyeclib's own bench: src/pyeclib/cli/bench.py
+:68-99).  Objects are independent, so N GPUs each take their own batch of
+256 (weak scaling, no collective on the data path).
+
+`roofline` covers the kernel that dominates a step (achieved = algorithmic
+bytes per launch / mean launch time from HIP events on the launch stream);
+`cpu_baseline` times the scalar C oracle (tests-only restatement of
+liberasurecode_rs_vand) on rank 0, single thread, over one full step's work.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident encode+decode GiB/s, k=10 m=4, 4 MiB objects, 1/2/4/8 GPU"
+SEED = 20261015
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="objects per GPU")
+    ap.add_argument("--obj-bytes", type=int, default=4 * 1024 * 1024)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--erasures", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=0,
+                    help="objects in the CPU baseline sample (default: the full batch)")
+    ap.add_argument("--host", action="store_true",
+                    help="also time the host-resident (pinned H2D/D2H) encode path")
+    ap.add_argument("--verify", action="store_true", help="check one object against the oracle")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    return world, rank, local
+
+
+def erasure_masks(rng, n_obj, k, m, erasures):
+    full = (1 << (k + m)) - 1
+    masks = []
+    for _ in range(n_obj):
+        lost = rng.choice(k + m, size=erasures, replace=False)
+        masks.append(full & ~int(sum(1 << int(i) for i in lost)))
+    return masks
+
+
+def cpu_baseline(args, host_objs, masks, sample):
+    """Scalar C oracle, one thread: encode + decode `sample` objects."""
+    import ctypes
+    from oracle import oracle as O
+    L = O.lib()
+    k, m, n = args.k, args.m, args.obj_bytes
+    fl = O.fragment_len(k, n)
+    out = np.zeros((k + m) * fl, dtype=np.uint8)
+    obj = np.zeros(n, dtype=np.uint8)
+    t_enc = t_dec = 0.0
+    for o in range(sample):
+        obj[:] = host_objs[o, :n]
+        t0 = time.perf_counter()
+        rc = L.orc_encode(k, m, O.CHKSUM_NONE, O.LIBEC_VERSION, obj.ctypes.data, n, out.ctypes.data)
+        t_enc += time.perf_counter() - t0
+        assert rc == 0
+        frags = [out[i * fl:(i + 1) * fl].tobytes() for i in range(k + m) if masks[o] >> i & 1]
+        arr = (ctypes.c_char_p * len(frags))(*frags)
+        dec = np.zeros(n, dtype=np.uint8)
+        olen = ctypes.c_uint64(0)
+        t0 = time.perf_counter()
+        rc = L.orc_decode(k, m, arr, len(frags), fl, dec.ctypes.data, ctypes.byref(olen))
+        t_dec += time.perf_counter() - t0
+        assert rc == 0 and olen.value == n
+    total = 2 * sample * n
+    return {
+        "value": round(total / (t_enc + t_dec) / 2**30, 4),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{sample} objects x {n} B: encode + decode with {args.erasures} erasures "
+                  f"each (one step's work for that many objects), scalar C oracle "
+                  f"(oracle/rs_vand_oracle.c), 1 thread",
+        "encode_GiBps": round(sample * n / t_enc / 2**30, 4),
+        "decode_GiBps": round(sample * n / t_dec / 2**30, 4),
+        "seconds": round(t_enc + t_dec, 2),
+    }
+
+
+def load_pmc(path):
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    import torch
+    from pyeclib_amd import batch
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    k, m, n, B = args.k, args.m, args.obj_bytes, args.batch
+    bs = batch.blocksize(k, n)
+    fs = batch.frag_stride(bs)
+    obj_stride = (n + 255) // 256 * 256
+
+    rng = np.random.Generator(np.random.PCG64(SEED + rank))
+    host = np.zeros((B, obj_stride), dtype=np.uint8)
+    host[:, :n] = rng.integers(0, 256, size=(B, n), dtype=np.uint8)
+    masks = erasure_masks(rng, B, k, m, args.erasures)
+
+    codec = batch.BatchCodec(k, m)
+    objs = torch.from_numpy(host).to(dev)
+    stripes = torch.zeros((B, k + m, fs), dtype=torch.uint8, device=dev)
+    out = torch.zeros((B, obj_stride), dtype=torch.uint8, device=dev)
+    # decode inputs: full stripes (data fragments materialised once, untimed)
+    codec.encode(objs, n, parity=stripes[:, k:], data=stripes[:, :k])
+    torch.cuda.synchronize()
+
+    if args.verify and rank == 0:
+        from oracle import oracle as O
+        want = O.encode(k, m, host[0, :n].tobytes())
+        got = stripes[0, :, :80 + bs].cpu().numpy()
+        assert all(got[i].tobytes() == want[i] for i in range(k + m)), "encode mismatch"
+        codec.decode(stripes, n, masks, out)
+        torch.cuda.synchronize()
+        assert torch.equal(out[:, :n].cpu(), torch.from_numpy(host[:, :n])), "decode mismatch"
+
+    stream = torch.cuda.current_stream()
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        codec.encode(objs, n, parity=stripes[:, k:])
+        if ev is not None:
+            ev[1].record(stream)
+        codec.decode(stripes, n, masks, out)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
+    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+    step_s = elapsed / args.steps
+    total_bytes = 2 * B * n * world
+    value = total_bytes / step_s / 2**30
+
+    # algorithmic HBM bytes per launch (DESIGN.md "Roofline"):
+    #   encode: read the object (L), write m payloads + m headers
+    #   decode: read k payloads, write the object
+    enc_bytes = B * (n + m * (bs + 80))
+    dec_bytes = B * (k * bs + n)
+    kernels = {
+        "encode": {"ms": round(enc_ms, 4), "bytes": enc_bytes,
+                   "GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1)},
+        "decode": {"ms": round(dec_ms, 4), "bytes": dec_bytes,
+                   "GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1)},
+    }
+    dom = "decode" if dec_ms >= enc_ms else "encode"
+    pmc = load_pmc(os.path.join(ROOT, "profiles", "pmc_summary.json")) or {}
+    traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
+    achieved = kernels[dom]["GBps"]
+    roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "algorithmic_bytes": kernels[dom]["bytes"]}
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u16",
+        "data": f"synthetic: PCG64(seed {SEED}+rank) uniform bytes; {args.erasures} random "
+                "erasures per object for decode",
+        "config": {"workload": f"rs_vand k={k} m={m} encode + decode ({args.erasures} erasures), "
+                               f"{n} B objects, batch {B} per GPU, device-resident",
+                   "k": k, "m": m, "object_bytes": n, "batch_per_gpu": B,
+                   "erasures": args.erasures, "parallelism": f"objects sharded over {world} GPU"},
+        "encode_GiBps": round(B * n * world / (enc_ms * 1e-3) / 2**30, 3),
+        "decode_GiBps": round(B * n * world / (dec_ms * 1e-3) / 2**30, 3),
+        "kernels": kernels,
+        "roofline": roofline,
+    }
+
+    if args.host and rank == 0:
+        pinned = torch.from_numpy(host).pin_memory()
+        hpar = torch.zeros((B, m, fs), dtype=torch.uint8).pin_memory()
+        codec.encode_host(pinned, n, hpar)
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            codec.encode_host(pinned, n, hpar)
+        th = (time.perf_counter() - t0) / reps
+        result["host_resident_encode_GiBps"] = round(B * n / th / 2**30, 3)
+
+    if rank == 0 and not args.no_cpu_baseline:
+        sample = args.cpu_sample or B
+        result["cpu_baseline"] = cpu_baseline(args, host, masks, min(sample, B))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,104 @@
+"""Batched, device-resident entry points (the ecamd_* half of the C ABI).
+
+Objects and fragments stay in HBM; only per-object erasure bitmasks cross
+from the host.  Buffers are anything exposing ``data_ptr()`` (torch tensors)
+or raw integer device addresses, laid out as documented in
+include/erasurecode_amd.h.  PyTorch is plumbing here (allocation, streams);
+it never touches the payload arithmetic.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Any, Sequence
+
+from . import _native
+
+HEADER = _native.HEADER_SIZE
+
+
+def blocksize(k: int, obj_len: int) -> int:
+    """Payload bytes per fragment: ceil(obj_len / 2k) * 2 (w = 16 alignment)."""
+    mult = 2 * k
+    return (obj_len + mult - 1) // mult * mult // k
+
+
+def frag_stride(bs: int) -> int:
+    """Smallest legal fragment slot: header + payload rounded to 16 bytes."""
+    return (HEADER + (bs + 15) // 16 * 16 + 15) // 16 * 16
+
+
+def _ptr(x: Any) -> int:
+    return int(x.data_ptr()) if hasattr(x, "data_ptr") else int(x)
+
+
+def _stride0(x: Any, default: int) -> int:
+    """Byte stride between objects of a (n_obj, ...) uint8 tensor."""
+    return int(x.stride(0)) if hasattr(x, "stride") else default
+
+
+def _stream(stream: Any) -> int | None:
+    if stream is None:
+        try:
+            import torch
+            return torch.cuda.current_stream().cuda_stream
+        except Exception:
+            return None
+    return int(getattr(stream, "cuda_stream", stream))
+
+
+class BatchCodec:
+    """One (k, m) rs_vand instance driving the batch kernels."""
+
+    def __init__(self, k: int, m: int, inline_crc32: bool = False):
+        self.k, self.m = k, m
+        self.handle = _native.init(k, m, 11, m, 1 if inline_crc32 else 0, 0, 0, 0)
+
+    def _check(self, ret: int, fn: str) -> None:
+        if ret < 0:
+            _native.raise_error(ret, fn)
+
+    def encode(self, objs: Any, obj_len: int, parity: Any, data: Any = None,
+               frag_stride: int | None = None, stream: Any = None) -> None:
+        """objs: (n_obj, obj_stride) uint8; parity: (n_obj, m, frag_stride)
+        (a view into a (n_obj, k+m, frag_stride) stripe buffer works);
+        data: optional (n_obj, k, frag_stride) view for materialised data
+        fragments."""
+        n_obj = int(objs.shape[0])
+        fs = frag_stride if frag_stride is not None else int(parity.stride(1))
+        ret = _native.lib.ecamd_encode_batch(
+            self.handle.desc, _ptr(objs), _stride0(objs, obj_len), obj_len, n_obj,
+            _ptr(parity), _ptr(data) if data is not None else None, fs,
+            _stride0(parity, self.m * fs), _stream(stream))
+        self._check(ret, "ecamd_encode_batch")
+
+    def decode(self, frags: Any, obj_len: int, avail_masks: Sequence[int], out: Any,
+               stream: Any = None) -> None:
+        """frags: (n_obj, k+m, frag_stride) stripes; out: (n_obj, obj_stride)."""
+        n_obj = len(avail_masks)
+        masks = (ctypes.c_uint32 * n_obj)(*avail_masks)
+        fs = int(frags.stride(1))
+        ret = _native.lib.ecamd_decode_batch(
+            self.handle.desc, _ptr(frags), fs, _stride0(frags, (self.k + self.m) * fs), obj_len,
+            n_obj, masks, _ptr(out), _stride0(out, obj_len), _stream(stream))
+        self._check(ret, "ecamd_decode_batch")
+
+    def reconstruct(self, frags: Any, obj_len: int, avail_masks: Sequence[int],
+                    dest: Sequence[int], out: Any, stream: Any = None) -> None:
+        """Rebuild fragment dest[o] of each object into out[o] (header included)."""
+        n_obj = len(avail_masks)
+        masks = (ctypes.c_uint32 * n_obj)(*avail_masks)
+        dst = (ctypes.c_int * n_obj)(*dest)
+        fs = int(frags.stride(1))
+        ret = _native.lib.ecamd_reconstruct_batch(
+            self.handle.desc, _ptr(frags), fs, _stride0(frags, (self.k + self.m) * fs), obj_len,
+            n_obj, masks, dst, _ptr(out), _stride0(out, fs), _stream(stream))
+        self._check(ret, "ecamd_reconstruct_batch")
+
+    def encode_host(self, objs: Any, obj_len: int, parity: Any) -> None:
+        """Host-resident encode: objs (n_obj, obj_stride) and parity
+        (n_obj, m, frag_stride) in (pinned) host memory."""
+        n_obj = int(objs.shape[0])
+        ret = _native.lib.ecamd_encode_host_batch(
+            self.handle.desc, _ptr(objs), _stride0(objs, obj_len), obj_len, n_obj,
+            _ptr(parity), int(parity.stride(1)))
+        self._check(ret, "ecamd_encode_host_batch")
