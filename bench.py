@@ -143,7 +143,7 @@ def main():
 
     codec = batch.BatchCodec(k, m)
     objs = torch.from_numpy(host).to(dev)
-    stripes = torch.zeros((B, k + m, fs), dtype=torch.uint8, device=dev)
+    stripes = batch.stripe_buffer(B, k, m, bs, device=dev)
     out = torch.zeros((B, obj_stride), dtype=torch.uint8, device=dev)
     # decode inputs: full stripes (data fragments materialised once, untimed)
     codec.encode(objs, n, parity=stripes[:, k:], data=stripes[:, :k])

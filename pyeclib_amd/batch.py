@@ -22,9 +22,26 @@ def blocksize(k: int, obj_len: int) -> int:
     return (obj_len + mult - 1) // mult * mult // k
 
 
-def frag_stride(bs: int) -> int:
-    """Smallest legal fragment slot: header + payload rounded to 16 bytes."""
-    return (HEADER + (bs + 15) // 16 * 16 + 15) // 16 * 16
+def frag_stride(bs: int, align: int = 128) -> int:
+    """Fragment slot size: header + payload (rounded to 16 B), rounded up to
+    `align` bytes.  With 128 and fragments starting PAYLOAD_SKEW bytes into a
+    128-B-aligned buffer, every payload starts on a 128-B cache line."""
+    return (HEADER + (bs + 15) // 16 * 16 + align - 1) // align * align
+
+
+# Fragment buffers start this many bytes past a 128-B boundary so that the
+# payload (after the 80-byte header) is line-aligned: 48 + 80 = 128.
+PAYLOAD_SKEW = 48
+
+
+def stripe_buffer(n_obj: int, k: int, m: int, bs: int, device: Any = None) -> Any:
+    """(n_obj, k+m, frag_stride) uint8 torch view whose payloads are 128-B aligned."""
+    import torch
+    fs = frag_stride(bs)
+    flat = torch.zeros(n_obj * (k + m) * fs + 128, dtype=torch.uint8, device=device)
+    base = flat.data_ptr() % 128
+    off = (PAYLOAD_SKEW - base) % 128
+    return flat[off:off + n_obj * (k + m) * fs].view(n_obj, k + m, fs)
 
 
 def _ptr(x: Any) -> int:

@@ -29,6 +29,8 @@
 // the loads rely on gfx9's unaligned-access mode for those inputs.
 #include "ec_kernels.hpp"
 
+#include <cstdlib>
+
 namespace ecamd {
 namespace {
 
@@ -52,6 +54,22 @@ __device__ __forceinline__ uint32_t lds_u32(uint32_t a, uint32_t tab) {
   return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
       reinterpret_cast<const lds_char*>(static_cast<uintptr_t>(a)) + tab);
 }
+// Streaming global accesses: every input byte is read once and every output
+// byte written once, so they bypass cache residency (nontemporal).  Measured
+// on the encode stream pattern (tools/microbench.hip): 4.9 -> 5.5 TB/s.
+__device__ __forceinline__ uint4 ld_stream(const void* p) {
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_stream(void* p, const uint4& x) {
+  v4u v;
+  v.x = x.x;
+  v.y = x.y;
+  v.z = x.z;
+  v.w = x.w;
+  __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
+}
+
 // a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -163,184 +181,290 @@ __device__ __forceinline__ int64_t object_bytes(uint32_t idx, uint32_t bs, uint3
   return n;
 }
 
-// ---------------- encode ----------------
+// ---------------- work decomposition ----------------
+//
+// Work item = (object o, tile of 256 lane chunks = 4 KiB of payload
+// positions).  Tiles [0, first_edge) of every object are "interior": all
+// lanes read 16 in-bounds bytes from every input and write 16 bytes to every
+// output, so the main kernels run them with no bounds checks, unrolled over
+// K and with the next item's loads in flight (register double buffering).
+// Tiles [first_edge, tiles) -- at most two per object: the payload tail and
+// the tile reaching the zero padding / the end of the object -- run in a
+// separate launch with a rolled, bounds-checked loop, so their code adds no
+// registers to the main kernels.
 
-// Edge lane of an encode tile: payload tail (t + 16 > bs) or a chunk that
-// reaches the zero padding past obj_len.  Rare; a rolled loop so that it
-// adds no registers to the unrolled interior path.
-template <int NW>
-__device__ __forceinline__ void encode_edge(const EncodeParams& p, uint32_t o, uint32_t t) {
-  const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride;
-  uint2 s[8];
-  for (int i = 0; i < 8; ++i) s[i] = make_uint2(0, 0);
-  const int64_t rem = static_cast<int64_t>(p.bs) - t;
-#pragma unroll 1
-  for (uint32_t j = 0; j < p.k; ++j) {
-    const uint4 x = load_clamped(obj, static_cast<uint64_t>(j) * p.bs + t, p.obj_len);
-    mac_chunk<NW>(j * kTableBytesPerInput, x, s);
-    if (p.data != nullptr && p.row0 == 0)
-      store_partial(p.data + static_cast<uint64_t>(o) * p.stripe_stride + j * p.frag_stride + kHeaderBytes + t,
-                    x, rem);
-  }
-  pin(s);
-  uint8_t* par = p.parity + static_cast<uint64_t>(o) * p.stripe_stride +
-                 p.row0 * p.frag_stride + kHeaderBytes + t;
-  for (uint32_t r = 0; r < p.nrows; ++r) store_partial(par + r * p.frag_stride, row_chunk(s, r), rem);
+__device__ __forceinline__ void tile_of(uint32_t w, uint32_t per_obj, uint32_t first,
+                                        uint32_t& o, uint32_t& tile, uint32_t& t) {
+  o = w / per_obj;
+  tile = first + (w - o * per_obj);
+  t = (tile * kThreadsPerBlock + threadIdx.x) << 4;
 }
 
+// ---------------- encode ----------------
+
+__device__ __forceinline__ void encode_headers(const EncodeParams& p, uint32_t o, uint32_t k) {
+  if (p.headers == nullptr) return;
+  if (p.row0 == 0)
+    copy_headers(p.parity + static_cast<uint64_t>(o) * p.stripe_stride, p.frag_stride,
+                 p.headers + k * kHeaderBytes, p.m);
+  if (p.data != nullptr)
+    copy_headers(p.data + static_cast<uint64_t>(o) * p.stripe_stride, p.frag_stride, p.headers,
+                 k);
+}
+
+template <int K>
+__device__ __forceinline__ void encode_load(const EncodeParams& p, uint32_t o, uint32_t t,
+                                            uint4 (&x)[K]) {
+  const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride + t;
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    x[j] = ld_stream(obj + static_cast<uint64_t>(j) * p.bs);
+}
+
+// One interior item with its inputs already in `cur`; first issues the loads
+// of the workgroup's next item into `nxt`, so they are in flight while this
+// item's table lookups run.
 template <int K, int NW>
-__global__ void __launch_bounds__(kThreadsPerBlock) encode_kernel(EncodeParams p) {
+__device__ __forceinline__ void encode_item(const EncodeParams& p, uint32_t w, uint32_t items,
+                                            uint4 (&cur)[K], uint4 (&nxt)[K]) {
+  uint32_t o, tile, t;
+  tile_of(w, p.first_edge, 0, o, tile, t);
+  const uint32_t wn = w + gridDim.x;
+  if (wn < items) {
+    uint32_t on, tn, ttn;
+    tile_of(wn, p.first_edge, 0, on, tn, ttn);
+    encode_load<K>(p, on, ttn, nxt);
+  }
+  if (tile == 0) encode_headers(p, o, K);
+  uint2 s[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = make_uint2(0, 0);
+#pragma unroll
+  for (int j = 0; j < K; ++j) mac_chunk<NW>(j * kTableBytesPerInput, cur[j], s);
+  pin(s);
+
+  uint8_t* par = p.parity + static_cast<uint64_t>(o) * p.stripe_stride + p.row0 * p.frag_stride +
+                 kHeaderBytes + t;
+#pragma unroll
+  for (int r = 0; r < kRowsPerPass; ++r)
+    if (r < static_cast<int>(p.nrows))
+      st_stream(par + r * p.frag_stride, row_chunk(s, r));
+
+  if (p.data != nullptr && p.row0 == 0) {
+    uint8_t* dat = p.data + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
+#pragma unroll
+    for (int j = 0; j < K; ++j) st_stream(dat + j * p.frag_stride, cur[j]);
+  }
+}
+
+template <int K, int NW, int MINW = 1, bool PIPE = true>
+__global__ void __launch_bounds__(kThreadsPerBlock, MINW) encode_kernel(EncodeParams p) {
   load_tables(p.tables, K);
   __syncthreads();
+  const uint32_t items = p.n_obj * p.first_edge;
+  if constexpr (!PIPE) {
+    // no cross-item prefetch: fewer VGPRs, more resident waves instead
+    for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
+      uint4 x[K];
+      uint32_t o, tile, t;
+      tile_of(w, p.first_edge, 0, o, tile, t);
+      encode_load<K>(p, o, t, x);
+      encode_item<K, NW>(p, w, 0, x, x);
+    }
+    return;
+  }
+  uint4 xa[K], xb[K];
+  uint32_t w = blockIdx.x;
+  if (w < items) {
+    uint32_t o, tile, t;
+    tile_of(w, p.first_edge, 0, o, tile, t);
+    encode_load<K>(p, o, t, xa);
+  }
+  while (w < items) {
+    encode_item<K, NW>(p, w, items, xa, xb);
+    w += gridDim.x;
+    if (w >= items) break;
+    encode_item<K, NW>(p, w, items, xb, xa);
+    w += gridDim.x;
+  }
+}
 
-  const uint32_t bs = p.bs;
-  const uint32_t chunks = (bs + 15) >> 4;
-  const uint32_t tiles = (chunks + kThreadsPerBlock - 1) / kThreadsPerBlock;
-  const uint32_t items = p.n_obj * tiles;
-  // Tiles whose every lane reads 16 in-object bytes from all K inputs and
-  // writes 16 payload bytes: t_end <= bs and (K-1)*bs + t_end <= obj_len.
-  const uint64_t tail_room = p.obj_len - static_cast<uint64_t>(K - 1) * bs;  // bytes of the last fragment in the object
+// Edge tiles: payload tail (t + 16 > bs) and chunks reaching the zero padding
+// past obj_len (liberasurecode's prepare_fragments_for_encode zero-fills).
+template <int NW>
+__global__ void __launch_bounds__(kThreadsPerBlock) encode_edge_kernel(EncodeParams p) {
+  load_tables(p.tables, p.k);
+  __syncthreads();
+  const uint32_t n_edge = p.tiles - p.first_edge;
+  const uint32_t items = p.n_obj * n_edge;
   for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
-    const uint32_t o = w / tiles;
-    const uint32_t tile = w - o * tiles;
-    if (tile == 0 && p.headers != nullptr) {
-      if (p.row0 == 0)
-        copy_headers(p.parity + static_cast<uint64_t>(o) * p.stripe_stride, p.frag_stride,
-                     p.headers + K * kHeaderBytes, p.m);
-      if (p.data != nullptr)
-        copy_headers(p.data + static_cast<uint64_t>(o) * p.stripe_stride, p.frag_stride,
-                     p.headers, K);
-    }
-    const uint32_t t = (tile * kThreadsPerBlock + threadIdx.x) << 4;
-    const uint32_t t_end = (tile + 1) * kThreadsPerBlock * 16;
-    if (t_end > bs || t_end > tail_room) {
-      if (t < bs) encode_edge<NW>(p, o, t);
-      continue;
-    }
-    const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride + t;
-
-    uint4 x[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-      x[j] = *reinterpret_cast<const uint4*>(obj + static_cast<uint64_t>(j) * bs);
-
+    uint32_t o, tile, t;
+    tile_of(w, n_edge, p.first_edge, o, tile, t);
+    if (tile == 0) encode_headers(p, o, p.k);
+    if (t >= p.bs) continue;
+    const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride;
+    const int64_t rem = static_cast<int64_t>(p.bs) - t;
     uint2 s[8];
-#pragma unroll
     for (int i = 0; i < 8; ++i) s[i] = make_uint2(0, 0);
-#pragma unroll
-    for (int j = 0; j < K; ++j) mac_chunk<NW>(j * kTableBytesPerInput, x[j], s);
+#pragma unroll 1
+    for (uint32_t j = 0; j < p.k; ++j) {
+      const uint4 x = load_clamped(obj, static_cast<uint64_t>(j) * p.bs + t, p.obj_len);
+      mac_chunk<NW>(j * kTableBytesPerInput, x, s);
+      if (p.data != nullptr && p.row0 == 0)
+        store_partial(p.data + static_cast<uint64_t>(o) * p.stripe_stride + j * p.frag_stride +
+                          kHeaderBytes + t,
+                      x, rem);
+    }
     pin(s);
-
     uint8_t* par = p.parity + static_cast<uint64_t>(o) * p.stripe_stride +
                    p.row0 * p.frag_stride + kHeaderBytes + t;
-#pragma unroll
-    for (int r = 0; r < kRowsPerPass; ++r)
-      if (r < static_cast<int>(p.nrows))
-        *reinterpret_cast<uint4*>(par + r * p.frag_stride) = row_chunk(s, r);
-
-    if (p.data != nullptr && p.row0 == 0) {
-      uint8_t* dat = p.data + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
-#pragma unroll
-      for (int j = 0; j < K; ++j) *reinterpret_cast<uint4*>(dat + j * p.frag_stride) = x[j];
-    }
+    for (uint32_t r = 0; r < p.nrows; ++r)
+      store_partial(par + r * p.frag_stride, row_chunk(s, r), rem);
   }
 }
 
 // ---------------- decode / reconstruct ----------------
 
-// Edge lane of a decode tile: payload tail or an output that crosses obj_len.
-template <int NW>
-__device__ __forceinline__ void decode_edge(const DecodeParams& p, const ObjDesc& d, uint32_t o,
-                                         uint32_t t) {
+// (Re)load the table set of object o's descriptor if it differs from the one
+// in LDS.  Workgroup-uniform; contains barriers.
+__device__ __forceinline__ void ensure_tables(const DecodeParams& p, const ObjDesc& d,
+                                              uint32_t& cur_table) {
+  if (d.n_out == 0 || d.table == cur_table) return;
+  __syncthreads();
+  load_tables(p.tables + static_cast<uint64_t>(d.table) * p.k * (kTableBytesPerInput / 8), p.k);
+  __syncthreads();
+  cur_table = d.table;
+}
+
+__device__ __forceinline__ void reconstruct_header(const DecodeParams& p, const ObjDesc& d,
+                                                   uint8_t* out) {
+  if (threadIdx.x < 5)
+    reinterpret_cast<uint4*>(out)[threadIdx.x] = reinterpret_cast<const uint4*>(
+        p.headers + static_cast<uint64_t>(d.header) * kHeaderBytes)[threadIdx.x];
+}
+
+template <int K>
+__device__ __forceinline__ void decode_load(const DecodeParams& p, uint32_t o, uint32_t t,
+                                            uint4 (&x)[K]) {
+  const ObjDesc& d = p.desc[o];
   const uint8_t* frags = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
-  uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
-  uint2 s[8];
-  for (int i = 0; i < 8; ++i) s[i] = make_uint2(0, 0);
-#pragma unroll 1
-  for (uint32_t j = 0; j < p.k; ++j) {
-    const uint4 x = *reinterpret_cast<const uint4*>(frags + d.in_idx[j] * p.frag_stride);
-    const uint32_t idx = d.in_idx[j];
-    if (d.copy_inputs && idx < p.k) {
-      const int64_t n = object_bytes(idx, p.bs, t, p.obj_len);
-      if (n > 0) store_partial(out + static_cast<uint64_t>(idx) * p.bs + t, x, n);
-    }
-    if (d.n_out) mac_chunk<NW>(j * kTableBytesPerInput, x, s);
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    x[j] = ld_stream(frags + d.in_idx[j] * p.frag_stride);
+}
+
+// One interior decode / reconstruct item with inputs in `cur`; prefetches
+// the workgroup's next item (w + step) into `nxt`.  Items are grid-strided
+// (the chip works on a few objects at a time: better DRAM locality than
+// contiguous per-workgroup ranges, measured 513 -> 479 us at k=10 m=4), so
+// the LDS tables are usually reloaded per item (5 KiB from L2).
+template <int K, int NW>
+__device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, uint32_t step,
+                                            uint32_t end, uint32_t& cur_table, uint4 (&cur)[K],
+                                            uint4 (&nxt)[K]) {
+  const uint32_t bs = p.bs;
+  uint32_t o, tile, t;
+  tile_of(w, p.first_edge, 0, o, tile, t);
+  if (w + step < end) {
+    uint32_t on, tn, ttn;
+    tile_of(w + step, p.first_edge, 0, on, tn, ttn);
+    decode_load<K>(p, on, ttn, nxt);
   }
-  pin(s);
-  for (uint32_t r = 0; r < d.n_out; ++r) {
-    if (p.reconstruct) {
-      store_partial(out + kHeaderBytes + t, row_chunk(s, r), static_cast<int64_t>(p.bs) - t);
-    } else {
-      const uint32_t idx = d.out_idx[r];
-      const int64_t n = object_bytes(idx, p.bs, t, p.obj_len);
-      if (n > 0) store_partial(out + static_cast<uint64_t>(idx) * p.bs + t, row_chunk(s, r), n);
+  const ObjDesc& d = p.desc[o];
+  ensure_tables(p, d, cur_table);
+  uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
+  if (p.reconstruct && tile == 0) reconstruct_header(p, d, out);
+  if (d.copy_inputs) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t idx = d.in_idx[j];
+      if (idx < K) st_stream(out + static_cast<uint64_t>(idx) * bs + t, cur[j]);
     }
+  }
+  const uint32_t n_out = d.n_out;
+  if (n_out == 0) return;
+
+  uint2 s[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = make_uint2(0, 0);
+#pragma unroll
+  for (int j = 0; j < K; ++j) mac_chunk<NW>(j * kTableBytesPerInput, cur[j], s);
+  pin(s);
+
+#pragma unroll
+  for (int r = 0; r < kRowsPerPass; ++r) {
+    if (r >= static_cast<int>(n_out)) break;
+    uint8_t* dst = p.reconstruct ? out + kHeaderBytes + t
+                                 : out + static_cast<uint64_t>(d.out_idx[r]) * bs + t;
+    st_stream(dst, row_chunk(s, r));
   }
 }
 
-template <int K, int NW>
-__global__ void __launch_bounds__(kThreadsPerBlock) decode_kernel(DecodeParams p) {
-  const uint32_t bs = p.bs;
-  const uint32_t chunks = (bs + 15) >> 4;
-  const uint32_t tiles = (chunks + kThreadsPerBlock - 1) / kThreadsPerBlock;
-  const uint32_t items = p.n_obj * tiles;
+template <int K, int NW, int MINW = 1, bool STRIDE = true>
+__global__ void __launch_bounds__(kThreadsPerBlock, MINW) decode_kernel(DecodeParams p) {
+  const uint32_t items = p.n_obj * p.first_edge;
+  const uint32_t per = (items + gridDim.x - 1) / gridDim.x;
+  const uint32_t begin = STRIDE ? blockIdx.x : blockIdx.x * per;
+  const uint32_t end = STRIDE ? items : min(items, begin + per);
+  const uint32_t step = STRIDE ? gridDim.x : 1;
+  uint32_t cur_table = 0xFFFFFFFFu;
+  uint4 xa[K], xb[K];
+  uint32_t w = begin;
+  if (w < end) {
+    uint32_t o, tile, t;
+    tile_of(w, p.first_edge, 0, o, tile, t);
+    decode_load<K>(p, o, t, xa);
+  }
+  while (w < end) {
+    decode_item<K, NW>(p, w, step, end, cur_table, xa, xb);
+    w += step;
+    if (w >= end) break;
+    decode_item<K, NW>(p, w, step, end, cur_table, xb, xa);
+    w += step;
+  }
+}
+
+// Edge tiles of decode / reconstruct: payload tail, and (decode) outputs
+// that cross the end of the object.
+template <int NW>
+__global__ void __launch_bounds__(kThreadsPerBlock) decode_edge_kernel(DecodeParams p) {
+  const uint32_t n_edge = p.tiles - p.first_edge;
+  const uint32_t items = p.n_obj * n_edge;
   const uint32_t per = (items + gridDim.x - 1) / gridDim.x;
   const uint32_t begin = blockIdx.x * per;
   const uint32_t end = min(items, begin + per);
-  // decode writes into objects: the last data fragment may end early
-  const uint64_t tail_room =
-      p.reconstruct ? ~uint64_t(0) : p.obj_len - static_cast<uint64_t>(K - 1) * bs;
   uint32_t cur_table = 0xFFFFFFFFu;
-
   for (uint32_t w = begin; w < end; ++w) {
-    const uint32_t o = w / tiles;
-    const uint32_t tile = w - o * tiles;
+    uint32_t o, tile, t;
+    tile_of(w, n_edge, p.first_edge, o, tile, t);
     const ObjDesc& d = p.desc[o];
-    const uint32_t n_out = d.n_out;
-    if (n_out != 0 && d.table != cur_table) {
-      __syncthreads();
-      load_tables(p.tables + static_cast<uint64_t>(d.table) * K * (kTableBytesPerInput / 8), K);
-      __syncthreads();
-      cur_table = d.table;
-    }
+    ensure_tables(p, d, cur_table);
     uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
-    if (p.reconstruct && tile == 0 && threadIdx.x < 5)
-      reinterpret_cast<uint4*>(out)[threadIdx.x] = reinterpret_cast<const uint4*>(
-          p.headers + static_cast<uint64_t>(d.header) * kHeaderBytes)[threadIdx.x];
-    const uint32_t t = (tile * kThreadsPerBlock + threadIdx.x) << 4;
-    const uint32_t t_end = (tile + 1) * kThreadsPerBlock * 16;
-    if (t_end > bs || t_end > tail_room) {
-      if (t < bs) decode_edge<NW>(p, d, o, t);
-      continue;
-    }
-    const uint8_t* frags = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
-    uint4 x[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j)
-      x[j] = *reinterpret_cast<const uint4*>(frags + d.in_idx[j] * p.frag_stride);
-
-    if (d.copy_inputs) {
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const uint32_t idx = d.in_idx[j];
-        if (idx < K) *reinterpret_cast<uint4*>(out + static_cast<uint64_t>(idx) * bs + t) = x[j];
-      }
-    }
-    if (n_out == 0) continue;
-
+    if (p.reconstruct && tile == 0) reconstruct_header(p, d, out);
+    if (t >= p.bs) continue;
+    const uint8_t* frags =
+        p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
     uint2 s[8];
-#pragma unroll
     for (int i = 0; i < 8; ++i) s[i] = make_uint2(0, 0);
-#pragma unroll
-    for (int j = 0; j < K; ++j) mac_chunk<NW>(j * kTableBytesPerInput, x[j], s);
+#pragma unroll 1
+    for (uint32_t j = 0; j < p.k; ++j) {
+      const uint4 x = *reinterpret_cast<const uint4*>(frags + d.in_idx[j] * p.frag_stride);
+      const uint32_t idx = d.in_idx[j];
+      if (d.copy_inputs && idx < p.k) {
+        const int64_t n = object_bytes(idx, p.bs, t, p.obj_len);
+        if (n > 0) store_partial(out + static_cast<uint64_t>(idx) * p.bs + t, x, n);
+      }
+      if (d.n_out) mac_chunk<NW>(j * kTableBytesPerInput, x, s);
+    }
     pin(s);
-
-#pragma unroll
-    for (int r = 0; r < kRowsPerPass; ++r) {
-      if (r >= static_cast<int>(n_out)) break;
-      uint8_t* dst = p.reconstruct ? out + kHeaderBytes + t
-                                   : out + static_cast<uint64_t>(d.out_idx[r]) * bs + t;
-      *reinterpret_cast<uint4*>(dst) = row_chunk(s, r);
+    for (uint32_t r = 0; r < d.n_out; ++r) {
+      if (p.reconstruct) {
+        store_partial(out + kHeaderBytes + t, row_chunk(s, r), static_cast<int64_t>(p.bs) - t);
+      } else {
+        const uint32_t idx = d.out_idx[r];
+        const int64_t n = object_bytes(idx, p.bs, t, p.obj_len);
+        if (n > 0) store_partial(out + static_cast<uint64_t>(idx) * p.bs + t, row_chunk(s, r), n);
+      }
     }
   }
 }
@@ -359,24 +483,72 @@ int grid_for(const void* kernel, size_t lds_bytes, uint32_t items) {
   return static_cast<int>(items < resident ? (items ? items : 1) : resident);
 }
 
-template <int K, int NW>
-hipError_t launch_encode_k(const EncodeParams& p, hipStream_t stream) {
-  const size_t lds = K * kTableBytesPerInput;
-  const uint32_t items = p.n_obj * tiles_per_fragment(p.bs);
-  auto kern = encode_kernel<K, NW>;
+// Interior tiles per object: tiles whose 4 KiB of positions end at or before
+// min(bs, room), where room = payload bytes of the last data fragment that
+// lie inside the object (decode outputs / encode inputs stop there).
+inline void split_tiles(uint32_t bs, uint64_t obj_len, uint32_t k, bool whole_payload,
+                        uint32_t& tiles, uint32_t& first_edge) {
+  tiles = tiles_per_fragment(bs);
+  int64_t room = whole_payload ? static_cast<int64_t>(bs)
+                               : static_cast<int64_t>(obj_len) - static_cast<int64_t>(k - 1) * bs;
+  if (room > static_cast<int64_t>(bs)) room = bs;
+  if (room < 0) room = 0;
+  first_edge = static_cast<uint32_t>(room / (kThreadsPerBlock * 16));
+}
+
+int variant(const char* name) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : 0;
+}
+
+template <typename Kern, typename Params>
+hipError_t launch(Kern kern, const Params& p, size_t lds, uint32_t items, hipStream_t stream) {
+  if (items == 0) return hipSuccess;
   const int grid = grid_for(reinterpret_cast<const void*>(kern), lds, items);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreadsPerBlock), lds, stream, p);
   return hipGetLastError();
 }
 
 template <int K, int NW>
-hipError_t launch_decode_k(const DecodeParams& p, hipStream_t stream) {
+hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   const size_t lds = K * kTableBytesPerInput;
-  const uint32_t items = p.n_obj * tiles_per_fragment(p.bs);
-  auto kern = decode_kernel<K, NW>;
-  const int grid = grid_for(reinterpret_cast<const void*>(kern), lds, items);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreadsPerBlock), lds, stream, p);
-  return hipGetLastError();
+  split_tiles(p.bs, p.obj_len, K, false, p.tiles, p.first_edge);
+  hipError_t e;
+  if constexpr (K == 10) {
+    // tuning experiment: ECAMD_MINW = minimum waves per SIMD for the main kernel
+    const int minw = variant("ECAMD_MINW");
+    const bool pipe = variant("ECAMD_NOPIPE") == 0;
+    const uint32_t n = p.n_obj * p.first_edge;
+    if (!pipe && minw == 6) e = launch(encode_kernel<K, NW, 6, false>, p, lds, n, stream);
+    else if (!pipe && minw == 5) e = launch(encode_kernel<K, NW, 5, false>, p, lds, n, stream);
+    else if (!pipe) e = launch(encode_kernel<K, NW, 1, false>, p, lds, n, stream);
+    else if (minw == 3) e = launch(encode_kernel<K, NW, 3>, p, lds, n, stream);
+    else if (minw == 4) e = launch(encode_kernel<K, NW, 4>, p, lds, n, stream);
+    else e = launch(encode_kernel<K, NW>, p, lds, n, stream);
+  } else {
+    e = launch(encode_kernel<K, NW>, p, lds, p.n_obj * p.first_edge, stream);
+  }
+  if (e != hipSuccess) return e;
+  return launch(encode_edge_kernel<NW>, p, lds, p.n_obj * (p.tiles - p.first_edge), stream);
+}
+
+template <int K, int NW>
+hipError_t launch_decode_k(DecodeParams p, hipStream_t stream) {
+  const size_t lds = K * kTableBytesPerInput;
+  split_tiles(p.bs, p.obj_len, K, p.reconstruct != 0, p.tiles, p.first_edge);
+  hipError_t e;
+  if constexpr (K == 10) {
+    const int minw = variant("ECAMD_MINW");
+    if (variant("ECAMD_DCONTIG"))
+      e = launch(decode_kernel<K, NW, 1, false>, p, lds, p.n_obj * p.first_edge, stream);
+    else if (minw == 3) e = launch(decode_kernel<K, NW, 3>, p, lds, p.n_obj * p.first_edge, stream);
+    else if (minw == 4) e = launch(decode_kernel<K, NW, 4>, p, lds, p.n_obj * p.first_edge, stream);
+    else e = launch(decode_kernel<K, NW>, p, lds, p.n_obj * p.first_edge, stream);
+  } else {
+    e = launch(decode_kernel<K, NW>, p, lds, p.n_obj * p.first_edge, stream);
+  }
+  if (e != hipSuccess) return e;
+  return launch(decode_edge_kernel<NW>, p, lds, p.n_obj * (p.tiles - p.first_edge), stream);
 }
 
 template <int K>

@@ -40,6 +40,7 @@ struct EncodeParams {
   uint32_t row0, nrows;     // parity rows handled by this pass
   uint32_t bs;              // payload bytes per fragment
   uint32_t n_obj;
+  uint32_t tiles, first_edge;  // set by the launcher (ec_kernels.hip: split_tiles)
 };
 
 // Per-object decode / reconstruct descriptor (device memory).
@@ -70,6 +71,7 @@ struct DecodeParams {
   uint32_t bs;
   uint32_t n_obj;
   uint32_t reconstruct;     // 1 = write fragment payload + header
+  uint32_t tiles, first_edge;  // set by the launcher (ec_kernels.hip: split_tiles)
 };
 
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);

@@ -1,0 +1,297 @@
+// Microbenchmark for the encode hot loop: separates the memory stream from
+// the LDS/VALU work.  Not part of the product; built by `make -C tools`.
+//
+//   stream   : same loads/stores as encode (K x 16 B strided by bs, R x 16 B
+//              out per lane), XOR instead of GF products      -> HBM roof
+//   compute  : GF products on register data, no HBM traffic   -> LDS/VALU roof
+//   full     : the product encode kernel (via launch_encode)
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <algorithm>
+#include <vector>
+
+#include "../pyeclib_amd/csrc/ec_kernels.hip"
+
+using namespace ecamd;
+
+namespace {
+
+template <int K>
+__global__ void __launch_bounds__(256) stream_kernel(const uint8_t* objs, uint8_t* par,
+                                                     uint32_t bs, uint32_t n_obj,
+                                                     uint64_t obj_stride, uint64_t frag_stride,
+                                                     uint32_t tiles) {
+  const uint32_t items = n_obj * tiles;
+  for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
+    const uint32_t o = w / tiles, tile = w % tiles;
+    const uint32_t t = (tile * 256 + threadIdx.x) * 16;
+    const uint8_t* src = objs + o * obj_stride + t;
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = *reinterpret_cast<const uint4*>(src + uint64_t(j) * bs);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      acc.x ^= x[j].x; acc.y ^= x[j].y; acc.z ^= x[j].z; acc.w ^= x[j].w;
+    }
+    uint8_t* dst = par + o * 4 * frag_stride + 80 + t;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      *reinterpret_cast<uint4*>(dst + r * frag_stride) = acc;
+      acc.x += 1;
+    }
+  }
+}
+
+// Variants of the encode memory stream.  C = 16-B chunks per lane per input
+// (adjacent), CONTIG = contiguous item ranges per workgroup (else grid
+// stride), NT = nontemporal loads/stores.
+template <int K, int C, bool CONTIG, bool NT, bool NTS = NT>
+__global__ void __launch_bounds__(256) stream2_kernel(const uint8_t* objs, uint8_t* par,
+                                                      uint32_t bs, uint32_t n_obj,
+                                                      uint64_t obj_stride, uint64_t frag_stride,
+                                                      uint32_t tiles, uint32_t out_off) {
+  const uint32_t items = n_obj * tiles;
+  const uint32_t per = (items + gridDim.x - 1) / gridDim.x;
+  const uint32_t b0 = CONTIG ? blockIdx.x * per : blockIdx.x;
+  const uint32_t b1 = CONTIG ? min(items, b0 + per) : items;
+  const uint32_t st = CONTIG ? 1 : gridDim.x;
+  for (uint32_t w = b0; w < b1; w += st) {
+    const uint32_t o = w / tiles, tile = w % tiles;
+    const uint32_t t = (tile * 256 * C + threadIdx.x * C) * 16;
+    const uint8_t* src = objs + o * obj_stride + t;
+    uint4 x[K][C];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const uint4* a = reinterpret_cast<const uint4*>(src + uint64_t(j) * bs + c * 16);
+        if constexpr (NT) {
+          x[j][c].x = __builtin_nontemporal_load(&a->x);
+          x[j][c].y = __builtin_nontemporal_load(&a->y);
+          x[j][c].z = __builtin_nontemporal_load(&a->z);
+          x[j][c].w = __builtin_nontemporal_load(&a->w);
+        } else {
+          x[j][c] = *a;
+        }
+      }
+    uint8_t* dst = par + o * 4 * frag_stride + out_off + t;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        acc.x ^= x[j][c].x; acc.y ^= x[j][c].y; acc.z ^= x[j][c].z; acc.w ^= x[j][c].w;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        uint4* d = reinterpret_cast<uint4*>(dst + r * frag_stride + c * 16);
+        if constexpr (NTS) {
+          __builtin_nontemporal_store(acc.x, &d->x);
+          __builtin_nontemporal_store(acc.y, &d->y);
+          __builtin_nontemporal_store(acc.z, &d->z);
+          __builtin_nontemporal_store(acc.w, &d->w);
+        } else {
+          *d = acc;
+        }
+        acc.x += 1;
+      }
+    }
+  }
+}
+
+// Reference streams: plain 16 B/lane copy and read-only sweep.
+__global__ void __launch_bounds__(256) copy_kernel(const uint4* src, uint4* dst, uint64_t n) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
+    dst[i] = src[i];
+}
+__global__ void __launch_bounds__(256) read_kernel(const uint4* src, uint64_t n, uint32_t* sink) {
+  uint32_t acc = 0;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256) {
+    const uint4 v = src[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9E3779B9u) sink[0] = acc;
+}
+
+template <int K>
+__global__ void __launch_bounds__(256) compute_kernel(const uint64_t* tables, uint8_t* sink,
+                                                      uint32_t iters) {
+  load_tables(tables, K);
+  __syncthreads();
+  uint4 x[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    x[j] = make_uint4(threadIdx.x * 2654435761u + j, blockIdx.x ^ (j << 7), threadIdx.x + j * 77,
+                      blockIdx.x * 31 + j);
+  uint2 s[8];
+  for (int i = 0; i < 8; ++i) s[i] = make_uint2(0, 0);
+  for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int j = 0; j < K; ++j)  // opaque inputs: nothing hoists out of the loop
+      asm volatile("" : "+v"(x[j].x), "+v"(x[j].y), "+v"(x[j].z), "+v"(x[j].w));
+#pragma unroll
+    for (int j = 0; j < K; ++j) mac_chunk<2>(j * kTableBytesPerInput, x[j], s);
+    pin(s);
+  }
+  uint32_t v = 0;
+  for (int i = 0; i < 8; ++i) v ^= s[i].x ^ s[i].y;
+  if (v == 0x12345678u) sink[threadIdx.x] = 1;
+}
+
+#define CHECK(x)                                                          \
+  do {                                                                    \
+    hipError_t e_ = (x);                                                  \
+    if (e_ != hipSuccess) {                                               \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(1);                                                       \
+    }                                                                     \
+  } while (0)
+
+template <typename F>
+float time_ms(F f, int reps) {
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  f();
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) f();
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  return ms / reps;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  constexpr int K = 10;
+  const int m = 4;
+  const uint32_t n_obj = argc > 1 ? std::atoi(argv[1]) : 256;
+  const uint64_t L = argc > 2 ? std::atoll(argv[2]) : (4u << 20);
+  const uint32_t bs = static_cast<uint32_t>(((L + 2 * K - 1) / (2 * K)) * 2);
+  const uint64_t obj_stride = (L + 255) / 256 * 256;
+  const uint64_t fs = ((80 + (bs + 15) / 16 * 16) + 15) / 16 * 16;
+  uint8_t *objs, *par;
+  uint64_t* tables;
+  CHECK(hipMalloc(&objs, n_obj * obj_stride));
+  CHECK(hipMalloc(&par, n_obj * m * fs));
+  CHECK(hipMalloc(&tables, K * 64 * 8));
+  std::vector<uint64_t> ht(K * 64);
+  for (size_t i = 0; i < ht.size(); ++i) ht[i] = i * 0x9E3779B97F4A7C15ull;
+  CHECK(hipMemcpy(tables, ht.data(), ht.size() * 8, hipMemcpyHostToDevice));
+  CHECK(hipMemset(objs, 7, n_obj * obj_stride));
+
+  const double bytes = double(n_obj) * (L + m * (bs + 80.0));
+  const uint32_t tiles = (bs / 16) / 256;  // interior tiles only
+  int cus = 256;
+  CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const char* mode = argc > 3 ? argv[3] : "all";
+  auto want = [&](const char* m) { return !std::strcmp(mode, "all") || !std::strcmp(mode, m); };
+  if (want("copy")) {
+    const uint64_t n16 = n_obj * obj_stride / 16;
+    const uint64_t ncopy = std::min<uint64_t>(n16, n_obj * m * fs / 16);
+    const uint4* src4 = reinterpret_cast<const uint4*>(objs);
+    uint4* dst4 = reinterpret_cast<uint4*>(par);
+    uint32_t* sink = reinterpret_cast<uint32_t*>(par);
+    for (int per_cu : {4, 8}) {
+      const dim3 grid(cus * per_cu);
+      float ms = time_ms([&] {
+        hipLaunchKernelGGL(copy_kernel, grid, dim3(256), 0, 0, src4, dst4, ncopy);
+      }, 20);
+      const double b = 2.0 * ncopy * 16;
+      std::printf("copy    grid=%d/CU  %.1f us  %.1f GB/s\n", per_cu, ms * 1e3, b / (ms * 1e-3) / 1e9);
+      ms = time_ms([&] {
+        hipLaunchKernelGGL(read_kernel, grid, dim3(256), 0, 0, src4, n16, sink);
+      }, 20);
+      std::printf("read    grid=%d/CU  %.1f us  %.1f GB/s\n", per_cu, ms * 1e3,
+                  n16 * 16.0 / (ms * 1e-3) / 1e9);
+    }
+  }
+  for (int per_cu : {2, 4, 8}) {
+    if (!want("stream")) break;
+    float ms = time_ms([&] {
+      hipLaunchKernelGGL(stream_kernel<K>, dim3(cus * per_cu), dim3(256), 0, 0, objs, par, bs,
+                         n_obj, obj_stride, fs, tiles);
+    }, 20);
+    std::printf("stream  grid=%d/CU  %.1f us  %.1f GB/s\n", per_cu, ms * 1e3,
+                bytes / (ms * 1e-3) / 1e9);
+  }
+  // compute: same number of (input chunk x table) MACs as one encode batch
+  const uint64_t chunks = uint64_t(n_obj) * tiles * 256;  // lane-chunks of 16 B per input
+  if (want("stream2")) {
+    const uint64_t fs2 = (fs + 255) / 256 * 256;
+    auto run = [&](auto kern, int C, const char* name, uint32_t off, int per_cu) {
+      const uint32_t tl = (bs / 16) / (256 * C);
+      const dim3 grid(cus * per_cu);
+      float ms = time_ms([&] {
+        hipLaunchKernelGGL(kern, grid, dim3(256), 0, 0, objs, par, bs, n_obj, obj_stride, fs2, tl,
+                           off);
+      }, 20);
+      std::printf("stream2 %-22s off=%3u grid=%d/CU %.1f us %.1f GB/s\n", name, off, per_cu,
+                  ms * 1e3, bytes / (ms * 1e-3) / 1e9);
+    };
+    for (int pc : {4, 8}) {
+      run(stream2_kernel<K, 1, false, false, true>, 1, "C1 stride nt-store", 128, pc);
+      run(stream2_kernel<K, 1, false, true, false>, 1, "C1 stride nt-load", 128, pc);
+      run(stream2_kernel<K, 1, false, true, true>, 1, "C1 stride nt", 128, pc);
+      run(stream2_kernel<K, 2, false, true, true>, 2, "C2 stride nt", 128, pc);
+      run(stream2_kernel<K, 2, false, false, true>, 2, "C2 stride nt-store", 128, pc);
+    }
+    for (int pc : {4, 8}) {
+      if (!std::getenv("MB_ALL")) break;
+      for (uint32_t off : {80u, 128u}) {
+        run(stream2_kernel<K, 1, false, false>, 1, "C1 stride", off, pc);
+        run(stream2_kernel<K, 1, true, false>, 1, "C1 contig", off, pc);
+        run(stream2_kernel<K, 2, false, false>, 2, "C2 stride", off, pc);
+        run(stream2_kernel<K, 2, true, false>, 2, "C2 contig", off, pc);
+        run(stream2_kernel<K, 1, false, true>, 1, "C1 stride nt", off, pc);
+        run(stream2_kernel<K, 1, true, true>, 1, "C1 contig nt", off, pc);
+        run(stream2_kernel<K, 2, true, true>, 2, "C2 contig nt", off, pc);
+      }
+    }
+  }
+  for (int per_cu : {4, 8}) {
+    if (!want("compute")) break;
+    const uint32_t blocks = cus * per_cu;
+    const uint32_t iters = static_cast<uint32_t>(chunks / (uint64_t(blocks) * 256));
+    float ms = time_ms([&] {
+      hipLaunchKernelGGL(compute_kernel<K>, dim3(blocks), dim3(256), K * 512, 0, tables, par,
+                         iters);
+    }, 10);
+    std::printf("compute grid=%d/CU  %.1f us  (%u iters)\n", per_cu, ms * 1e3, iters);
+  }
+  EncodeParams p{};
+  p.objs = objs;
+  p.obj_stride = obj_stride;
+  p.obj_len = L;
+  p.parity = par;
+  p.frag_stride = fs;
+  p.stripe_stride = m * fs;
+  p.tables = tables;
+  p.k = K;
+  p.m = m;
+  p.row0 = 0;
+  p.nrows = m;
+  p.bs = bs;
+  p.n_obj = n_obj;
+  if (!want("full")) return 0;
+  float ms = time_ms([&] { CHECK(launch_encode(p, 0)); }, 20);
+  std::printf("full encode  payload%%128=80  %.1f us  %.1f GB/s\n", ms * 1e3, bytes / (ms * 1e-3) / 1e9);
+  // line-aligned payloads: fragment slots start 48 B into 256-B-aligned slots
+  const uint64_t fs_al = (80 + (bs + 15) / 16 * 16 + 48 + 255) / 256 * 256;
+  uint8_t* par2;
+  CHECK(hipMalloc(&par2, n_obj * m * fs_al + 256));
+  p.parity = par2 + 48;
+  p.frag_stride = fs_al;
+  p.stripe_stride = m * fs_al;
+  ms = time_ms([&] { CHECK(launch_encode(p, 0)); }, 20);
+  std::printf("full encode  payload%%128=0   %.1f us  %.1f GB/s\n", ms * 1e3, bytes / (ms * 1e-3) / 1e9);
+  return 0;
+}
