@@ -42,7 +42,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=256, help="objects per GPU")
+    ap.add_argument("--batch", type=int, default=256, help="objects per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="shard this many objects over the GPUs instead (strong scaling)")
     ap.add_argument("--obj-bytes", type=int, default=4 * 1024 * 1024)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--m", type=int, default=4)
@@ -54,17 +56,6 @@ def parse():
                     help="also time the host-resident (pinned H2D/D2H) encode path")
     ap.add_argument("--verify", action="store_true", help="check one object against the oracle")
     return ap.parse_args()
-
-
-def dist_setup(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    return world, rank, local
 
 
 def erasure_masks(rng, n_obj, k, m, erasures):
@@ -125,13 +116,19 @@ def load_pmc(path):
 
 def main():
     args = parse()
-    world, rank, local = dist_setup(args)
+    from pyeclib_amd import shard
+    world, rank, local = shard.init("nccl")
     import torch
     from pyeclib_amd import batch
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    k, m, n, B = args.k, args.m, args.obj_bytes, args.batch
+    k, m, n = args.k, args.m, args.obj_bytes
+    if args.global_batch:
+        lo, hi = shard.shard_range(args.global_batch, rank, world)
+        B = hi - lo
+    else:
+        B = args.batch
     bs = batch.blocksize(k, n)
     fs = batch.frag_stride(bs)
     obj_stride = (n + 255) // 256 * 256
@@ -175,26 +172,20 @@ def main():
     torch.cuda.synchronize()
 
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
+    shard.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(events[i])
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    shard.barrier()
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0, device=dev)
 
     enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
     step_s = elapsed / args.steps
-    total_bytes = 2 * B * n * world
+    n_total = args.global_batch or B * world
+    total_bytes = 2 * n_total * n
     value = total_bytes / step_s / 2**30
 
     # algorithmic HBM bytes per launch (DESIGN.md "Roofline"):
@@ -225,7 +216,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(step_s * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_batch else "weak",
         "vs_baseline": None,
         "dtype": "u16",
         "data": f"synthetic: PCG64(seed {SEED}+rank) uniform bytes; {args.erasures} random "
@@ -234,8 +225,8 @@ def main():
                                f"{n} B objects, batch {B} per GPU, device-resident",
                    "k": k, "m": m, "object_bytes": n, "batch_per_gpu": B,
                    "erasures": args.erasures, "parallelism": f"objects sharded over {world} GPU"},
-        "encode_GiBps": round(B * n * world / (enc_ms * 1e-3) / 2**30, 3),
-        "decode_GiBps": round(B * n * world / (dec_ms * 1e-3) / 2**30, 3),
+        "encode_GiBps": round(n_total * n / (enc_ms * 1e-3) / 2**30, 3),
+        "decode_GiBps": round(n_total * n / (dec_ms * 1e-3) / 2**30, 3),
         "kernels": kernels,
         "roofline": roofline,
     }
