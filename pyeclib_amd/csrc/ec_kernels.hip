@@ -353,12 +353,107 @@ __device__ __forceinline__ void decode_load(const DecodeParams& p, uint32_t o, u
     x[j] = ld_stream(frags + d.in_idx[j] * p.frag_stride);
 }
 
+// ---- output realignment for decode (objects) ----
+//
+// Decode writes data fragment j of object o to out + o*out_stride + j*bs,
+// and bs = 2*ceil(L/2k) leaves those slices at arbitrary (even) offsets
+// from a 128-B cache line, while the kernel's lanes are aligned to the
+// fragment payloads it reads.  Partial-line nontemporal stores measured 20%
+// slower than line-aligned ones (tools/microbench.hip, "dstream": 448 vs
+// 378 us).  So each output chunk is staged in LDS (one 4 KiB slot per
+// output, 4 slots) and re-read at the object's alignment: every wave then
+// writes whole 128-B lines except the two lines a tile shares with its
+// neighbours, which get byte stores of exactly the tile's own bytes.
+constexpr uint32_t kStageSlots = 4;
+constexpr uint32_t kStageBytes = kThreadsPerBlock * 16;  // one tile of one output
+
+__device__ __forceinline__ void lds_store16(uint32_t addr, const uint4& v) {
+  v4u w;
+  w.x = v.x;
+  w.y = v.y;
+  w.z = v.z;
+  w.w = v.w;
+  *reinterpret_cast<__attribute__((address_space(3))) v4u*>(static_cast<uintptr_t>(addr)) = w;
+}
+__device__ __forceinline__ uint32_t lds_u32_at(uint32_t addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+      static_cast<uintptr_t>(addr));
+}
+__device__ __forceinline__ uint2 lds_u64_at(uint32_t addr) {
+  const v2u v = *reinterpret_cast<const __attribute__((address_space(3))) v2u*>(
+      static_cast<uintptr_t>(addr));
+  return make_uint2(v.x, v.y);
+}
+
+// 16 bytes at an even LDS byte address (wave-uniform alignment class).
+__device__ __forceinline__ uint4 lds_read16_unaligned(uint32_t addr, uint32_t mis) {
+  if ((mis & 7) == 0) {
+    const uint2 a = lds_u64_at(addr), b = lds_u64_at(addr + 8);
+    return make_uint4(a.x, a.y, b.x, b.y);
+  }
+  if ((mis & 3) == 0)
+    return make_uint4(lds_u32_at(addr), lds_u32_at(addr + 4), lds_u32_at(addr + 8),
+                      lds_u32_at(addr + 12));
+  // 2 mod 4: five dwords, funnel-shifted by 16 bits
+  const uint32_t a = addr - 2;
+  const uint32_t d0 = lds_u32_at(a), d1 = lds_u32_at(a + 4), d2 = lds_u32_at(a + 8),
+                 d3 = lds_u32_at(a + 12), d4 = lds_u32_at(a + 16);
+  return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, 2), __builtin_amdgcn_alignbyte(d2, d1, 2),
+                    __builtin_amdgcn_alignbyte(d3, d2, 2), __builtin_amdgcn_alignbyte(d4, d3, 2));
+}
+
+// Slot destinations are packed 8 bits each into one register: a private
+// array here would be promoted to static LDS by hipcc, which would move the
+// dynamic LDS base away from address 0 (see launch()).
+struct Stager {
+  uint32_t base;  // LDS byte address of slot 0
+  uint32_t n;     // slots filled
+  uint32_t dest;  // destination fragment of slot q in bits 8q..8q+7
+};
+
+// Write every staged output back, line-aligned, then free the slots.  The
+// tile covers payload bytes [T, T + 4096) of each destination fragment.
+__device__ __forceinline__ void stage_flush(Stager& st, uint8_t* obj, uint32_t bs, uint32_t T) {
+  if (st.n == 0) return;
+  __syncthreads();
+  for (uint32_t q = 0; q < st.n; ++q) {
+    uint8_t* x0 = obj + static_cast<uint64_t>((st.dest >> (8 * q)) & 0xFFu) * bs + T;
+    const uint32_t delta = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(x0) & 127u);
+    uint8_t* a0 = x0 - delta;
+    const uint32_t slot = st.base + q * (kStageBytes + 128);
+    for (uint32_t c = threadIdx.x; c < kThreadsPerBlock + 8; c += kThreadsPerBlock) {
+      const int32_t off = static_cast<int32_t>(16 * c) - static_cast<int32_t>(delta);
+      if (off <= -16 || off >= static_cast<int32_t>(kStageBytes)) continue;
+      const uint4 v = lds_read16_unaligned(slot + 64 + off, delta);
+      if (off >= 0 && off + 16 <= static_cast<int32_t>(kStageBytes)) {
+        st_stream(a0 + 16 * c, v);
+      } else {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        for (int i = 0; i < 16; ++i)
+          if (off + i >= 0 && off + i < static_cast<int32_t>(kStageBytes))
+            a0[16 * c + i] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
+      }
+    }
+  }
+  __syncthreads();
+  st.n = 0;
+  st.dest = 0;
+}
+
+__device__ __forceinline__ void stage_put(Stager& st, const uint4& v, uint32_t dest,
+                                          uint8_t* obj, uint32_t bs, uint32_t T) {
+  if (st.n == kStageSlots) stage_flush(st, obj, bs, T);
+  lds_store16(st.base + st.n * (kStageBytes + 128) + 64 + 16 * threadIdx.x, v);
+  st.dest |= dest << (8 * st.n);
+  ++st.n;
+}
+
 // One interior decode / reconstruct item with inputs in `cur`; prefetches
 // the workgroup's next item (w + step) into `nxt`.  Items are grid-strided
 // (the chip works on a few objects at a time: better DRAM locality than
 // contiguous per-workgroup ranges, measured 513 -> 479 us at k=10 m=4), so
 // the LDS tables are usually reloaded per item (5 KiB from L2).
-template <int K, int NW>
+template <int K, int NW, bool STAGE>
 __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, uint32_t step,
                                             uint32_t end, uint32_t& cur_table, uint4 (&cur)[K],
                                             uint4 (&nxt)[K]) {
@@ -374,6 +469,33 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
   ensure_tables(p, d, cur_table);
   uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
   if (p.reconstruct && tile == 0) reconstruct_header(p, d, out);
+  const uint32_t n_out = d.n_out;
+
+  uint2 s[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = make_uint2(0, 0);
+  if (n_out != 0) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) mac_chunk<NW>(j * kTableBytesPerInput, cur[j], s);
+  }
+  pin(s);
+
+  if (STAGE && !p.reconstruct) {
+    const uint32_t T = tile * kStageBytes;
+    Stager st{static_cast<uint32_t>(K * kTableBytesPerInput), 0, 0};
+    if (d.copy_inputs) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const uint32_t idx = d.in_idx[j];
+        if (idx < K) stage_put(st, cur[j], idx, out, bs, T);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kRowsPerPass; ++r)
+      if (r < static_cast<int>(n_out)) stage_put(st, row_chunk(s, r), d.out_idx[r], out, bs, T);
+    stage_flush(st, out, bs, T);
+    return;
+  }
   if (d.copy_inputs) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
@@ -381,16 +503,6 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
       if (idx < K) st_stream(out + static_cast<uint64_t>(idx) * bs + t, cur[j]);
     }
   }
-  const uint32_t n_out = d.n_out;
-  if (n_out == 0) return;
-
-  uint2 s[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) s[i] = make_uint2(0, 0);
-#pragma unroll
-  for (int j = 0; j < K; ++j) mac_chunk<NW>(j * kTableBytesPerInput, cur[j], s);
-  pin(s);
-
 #pragma unroll
   for (int r = 0; r < kRowsPerPass; ++r) {
     if (r >= static_cast<int>(n_out)) break;
@@ -400,7 +512,7 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
   }
 }
 
-template <int K, int NW, int MINW = 1, bool STRIDE = true>
+template <int K, int NW, int MINW = 1, bool STRIDE = true, bool STAGE = true>
 __global__ void __launch_bounds__(kThreadsPerBlock, MINW) decode_kernel(DecodeParams p) {
   const uint32_t items = p.n_obj * p.first_edge;
   const uint32_t per = (items + gridDim.x - 1) / gridDim.x;
@@ -416,10 +528,10 @@ __global__ void __launch_bounds__(kThreadsPerBlock, MINW) decode_kernel(DecodePa
     decode_load<K>(p, o, t, xa);
   }
   while (w < end) {
-    decode_item<K, NW>(p, w, step, end, cur_table, xa, xb);
+    decode_item<K, NW, STAGE>(p, w, step, end, cur_table, xa, xb);
     w += step;
     if (w >= end) break;
-    decode_item<K, NW>(p, w, step, end, cur_table, xb, xa);
+    decode_item<K, NW, STAGE>(p, w, step, end, cur_table, xb, xa);
     w += step;
   }
 }
@@ -501,9 +613,23 @@ int variant(const char* name) {
   return v ? std::atoi(v) : 0;
 }
 
+// The kernels address LDS by raw byte offset from 0, which is only valid when
+// the kernel has no static __shared__ data (the dynamic allocation then
+// starts at address 0).  Checked once per kernel; a violation fails loudly.
+template <typename Kern>
+bool lds_starts_at_zero(Kern kern) {
+  static const bool ok = [kern] {
+    hipFuncAttributes attr{};
+    return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(kern)) == hipSuccess &&
+           attr.sharedSizeBytes == 0;
+  }();
+  return ok;
+}
+
 template <typename Kern, typename Params>
 hipError_t launch(Kern kern, const Params& p, size_t lds, uint32_t items, hipStream_t stream) {
   if (items == 0) return hipSuccess;
+  if (!lds_starts_at_zero(kern)) return hipErrorInvalidKernelFile;
   const int grid = grid_for(reinterpret_cast<const void*>(kern), lds, items);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreadsPerBlock), lds, stream, p);
   return hipGetLastError();
@@ -534,12 +660,16 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
 
 template <int K, int NW>
 hipError_t launch_decode_k(DecodeParams p, hipStream_t stream) {
-  const size_t lds = K * kTableBytesPerInput;
+  const size_t lds_tables = K * kTableBytesPerInput;
+  // + output staging slots (decode only), each with 64 B of slack either side
+  const size_t lds = lds_tables + (p.reconstruct ? 0 : kStageSlots * (kStageBytes + 128));
   split_tiles(p.bs, p.obj_len, K, p.reconstruct != 0, p.tiles, p.first_edge);
   hipError_t e;
   if constexpr (K == 10) {
     const int minw = variant("ECAMD_MINW");
-    if (variant("ECAMD_DCONTIG"))
+    if (variant("ECAMD_NOSTAGE"))
+      e = launch(decode_kernel<K, NW, 1, true, false>, p, lds, p.n_obj * p.first_edge, stream);
+    else if (variant("ECAMD_DCONTIG"))
       e = launch(decode_kernel<K, NW, 1, false>, p, lds, p.n_obj * p.first_edge, stream);
     else if (minw == 3) e = launch(decode_kernel<K, NW, 3>, p, lds, p.n_obj * p.first_edge, stream);
     else if (minw == 4) e = launch(decode_kernel<K, NW, 4>, p, lds, p.n_obj * p.first_edge, stream);
@@ -548,7 +678,7 @@ hipError_t launch_decode_k(DecodeParams p, hipStream_t stream) {
     e = launch(decode_kernel<K, NW>, p, lds, p.n_obj * p.first_edge, stream);
   }
   if (e != hipSuccess) return e;
-  return launch(decode_edge_kernel<NW>, p, lds, p.n_obj * (p.tiles - p.first_edge), stream);
+  return launch(decode_edge_kernel<NW>, p, lds_tables, p.n_obj * (p.tiles - p.first_edge), stream);
 }
 
 template <int K>

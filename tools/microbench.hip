@@ -104,6 +104,62 @@ __global__ void __launch_bounds__(256) stream2_kernel(const uint8_t* objs, uint8
   }
 }
 
+// Decode memory pattern: K aligned fragment payload reads -> K object slices.
+template <int K, bool NT>
+__global__ void __launch_bounds__(256) dstream_kernel(const uint8_t* frags, uint8_t* objs,
+                                                      uint32_t bs, uint32_t n_obj,
+                                                      uint64_t obj_stride, uint64_t fs,
+                                                      uint32_t tiles) {
+  const uint32_t items = n_obj * tiles;
+  for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
+    const uint32_t o = w / tiles, tile = w % tiles;
+    const uint32_t t = (tile * 256 + threadIdx.x) * 16;
+    const uint8_t* src = frags + o * (K + 4) * fs + 128 + t;
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint4* a = reinterpret_cast<const uint4*>(src + j * fs);
+      if constexpr (NT) x[j] = ld_stream(a); else x[j] = *a;
+    }
+    uint8_t* dst = objs + o * obj_stride + t;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      uint4* d = reinterpret_cast<uint4*>(dst + uint64_t(j) * bs);
+      if constexpr (NT) st_stream(d, x[j]); else *d = x[j];
+    }
+  }
+}
+
+// Same pattern with the copy realigned on the load side: each lane loads
+// fragment j at payload offset t - delta_j (unaligned) so that its store to
+// the object lands on a 16-B boundary and every wave writes whole lines.
+template <int K, bool NT>
+__global__ void __launch_bounds__(256) dstream_shift_kernel(const uint8_t* frags, uint8_t* objs,
+                                                            uint32_t bs, uint32_t n_obj,
+                                                            uint64_t obj_stride, uint64_t fs,
+                                                            uint32_t tiles) {
+  const uint32_t items = n_obj * tiles;
+  for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
+    const uint32_t o = w / tiles, tile = w % tiles;
+    const uint32_t t = (tile * 256 + threadIdx.x) * 16;
+    const uint8_t* src = frags + o * (K + 4) * fs + 128 + t;
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t delta = (j * bs) & 127u;
+      const uint4* a = reinterpret_cast<const uint4*>(src + j * fs - delta);
+      if constexpr (NT) x[j] = ld_stream(a); else x[j] = *a;
+    }
+    uint8_t* dst = objs + o * obj_stride + t;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t delta = (j * bs) & 127u;
+      uint4* d = reinterpret_cast<uint4*>(dst + uint64_t(j) * bs - delta);
+      if constexpr (NT) st_stream(d, x[j]); else *d = x[j];
+    }
+  }
+}
+
 // Reference streams: plain 16 B/lane copy and read-only sweep.
 __global__ void __launch_bounds__(256) copy_kernel(const uint4* src, uint4* dst, uint64_t n) {
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
@@ -225,6 +281,36 @@ int main(int argc, char** argv) {
   }
   // compute: same number of (input chunk x table) MACs as one encode batch
   const uint64_t chunks = uint64_t(n_obj) * tiles * 256;  // lane-chunks of 16 B per input
+  if (want("dstream")) {
+    const uint64_t fsd = (128 + (bs + 15) / 16 * 16 + 127) / 128 * 128;
+    uint8_t* frags;
+    CHECK(hipMalloc(&frags, n_obj * (K + 4) * fsd + 256));
+    const uint32_t tl = (bs / 16) / 256;
+    const double db = double(n_obj) * (2.0 * K * bs);
+    for (int per_cu : {4, 8}) {
+      const dim3 grid(cus * per_cu);
+      float ms = time_ms([&] {
+        hipLaunchKernelGGL((dstream_kernel<K, true>), grid, dim3(256), 0, 0, frags, objs, bs,
+                           n_obj, obj_stride, fsd, tl);
+      }, 20);
+      std::printf("dstream nt grid=%d/CU %.1f us %.1f GB/s\n", per_cu, ms * 1e3, db / (ms * 1e-3) / 1e9);
+      ms = time_ms([&] {
+        hipLaunchKernelGGL((dstream_kernel<K, false>), grid, dim3(256), 0, 0, frags, objs, bs,
+                           n_obj, obj_stride, fsd, tl);
+      }, 20);
+      std::printf("dstream    grid=%d/CU %.1f us %.1f GB/s\n", per_cu, ms * 1e3, db / (ms * 1e-3) / 1e9);
+      ms = time_ms([&] {
+        hipLaunchKernelGGL((dstream_shift_kernel<K, true>), grid, dim3(256), 0, 0, frags, objs,
+                           bs, n_obj, obj_stride, fsd, tl);
+      }, 20);
+      std::printf("dshift nt  grid=%d/CU %.1f us %.1f GB/s\n", per_cu, ms * 1e3, db / (ms * 1e-3) / 1e9);
+      ms = time_ms([&] {
+        hipLaunchKernelGGL((dstream_shift_kernel<K, false>), grid, dim3(256), 0, 0, frags, objs,
+                           bs, n_obj, obj_stride, fsd, tl);
+      }, 20);
+      std::printf("dshift     grid=%d/CU %.1f us %.1f GB/s\n", per_cu, ms * 1e3, db / (ms * 1e-3) / 1e9);
+    }
+  }
   if (want("stream2")) {
     const uint64_t fs2 = (fs + 255) / 256 * 256;
     auto run = [&](auto kern, int C, const char* name, uint32_t off, int per_cu) {

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 PMC passes of bench.py into profiles/pmc_summary.json.
+
+Usage (two separate passes: FETCH_SIZE and WRITE_SIZE do not fit one pass):
+  rocprofv3 --pmc FETCH_SIZE --output-format csv -d OUT/fetch -o run -- python3 bench.py ...
+  rocprofv3 --pmc WRITE_SIZE --output-format csv -d OUT/write -o run -- python3 bench.py ...
+  python3 tools/pmc_summary.py OUT/fetch OUT/write profiles/pmc_summary.json
+
+Per MI355X_MICROARCH.md §HBM: FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950
+FETCH_SIZE reports half the bytes of a wide coalesced streaming read, so it is
+doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  A "launch" here is one
+bench call (main kernel + its edge kernel), matching bench.py's events.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def load(path, counter):
+    files = glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)
+    per = defaultdict(lambda: defaultdict(float))  # op -> dispatch -> value
+    for f in files:
+        for row in csv.DictReader(open(f)):
+            if row["Counter_Name"] != counter:
+                continue
+            name = row["Kernel_Name"]
+            op = "encode" if "encode" in name else "decode" if "decode" in name else None
+            if op is None or "ecamd" not in name:
+                continue
+            per[op][(name, row["Dispatch_Id"])] += float(row["Counter_Value"])
+    out = {}
+    for op, d in per.items():
+        main = [v for (n, _), v in d.items() if "edge" not in n]
+        edge = [v for (n, _), v in d.items() if "edge" in n]
+        out[op] = (sum(main) / max(len(main), 1)) + (sum(edge) / max(len(edge), 1))
+    return out
+
+
+def main():
+    fetch_dir, write_dir, dst = sys.argv[1:4]
+    fetch = load(fetch_dir, "FETCH_SIZE")
+    write = load(write_dir, "WRITE_SIZE")
+    summary = {}
+    for op in sorted(set(fetch) | set(write)):
+        f_kib, w_kib = fetch.get(op, 0.0), write.get(op, 0.0)
+        summary[op] = {
+            "fetch_size_kib": round(f_kib, 1),
+            "write_size_kib": round(w_kib, 1),
+            "hbm_bytes_per_launch": int(round((2 * f_kib + w_kib) * 1024)),
+            "note": "2*FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE half-count correction)",
+        }
+    with open(dst, "w") as fh:
+        json.dump(summary, fh, indent=1)
+    print(json.dumps(summary))
+
+
+if __name__ == "__main__":
+    main()
