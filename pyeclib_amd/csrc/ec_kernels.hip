@@ -257,22 +257,11 @@ __device__ __forceinline__ void encode_item(const EncodeParams& p, uint32_t w, u
   }
 }
 
-template <int K, int NW, int MINW = 1, bool PIPE = true>
-__global__ void __launch_bounds__(kThreadsPerBlock, MINW) encode_kernel(EncodeParams p) {
+template <int K, int NW>
+__global__ void __launch_bounds__(kThreadsPerBlock) encode_kernel(EncodeParams p) {
   load_tables(p.tables, K);
   __syncthreads();
   const uint32_t items = p.n_obj * p.first_edge;
-  if constexpr (!PIPE) {
-    // no cross-item prefetch: fewer VGPRs, more resident waves instead
-    for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
-      uint4 x[K];
-      uint32_t o, tile, t;
-      tile_of(w, p.first_edge, 0, o, tile, t);
-      encode_load<K>(p, o, t, x);
-      encode_item<K, NW>(p, w, 0, x, x);
-    }
-    return;
-  }
   uint4 xa[K], xb[K];
   uint32_t w = blockIdx.x;
   if (w < items) {
@@ -343,117 +332,38 @@ __device__ __forceinline__ void reconstruct_header(const DecodeParams& p, const 
         p.headers + static_cast<uint64_t>(d.header) * kHeaderBytes)[threadIdx.x];
 }
 
+// Inputs are read through the cache (not nontemporal): decode reads the
+// surviving data fragments' lines again for the line-aligned copies below.
 template <int K>
 __device__ __forceinline__ void decode_load(const DecodeParams& p, uint32_t o, uint32_t t,
                                             uint4 (&x)[K]) {
   const ObjDesc& d = p.desc[o];
   const uint8_t* frags = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
 #pragma unroll
-  for (int j = 0; j < K; ++j)
-    x[j] = ld_stream(frags + d.in_idx[j] * p.frag_stride);
-}
-
-// ---- output realignment for decode (objects) ----
-//
-// Decode writes data fragment j of object o to out + o*out_stride + j*bs,
-// and bs = 2*ceil(L/2k) leaves those slices at arbitrary (even) offsets
-// from a 128-B cache line, while the kernel's lanes are aligned to the
-// fragment payloads it reads.  Partial-line nontemporal stores measured 20%
-// slower than line-aligned ones (tools/microbench.hip, "dstream": 448 vs
-// 378 us).  So each output chunk is staged in LDS (one 4 KiB slot per
-// output, 4 slots) and re-read at the object's alignment: every wave then
-// writes whole 128-B lines except the two lines a tile shares with its
-// neighbours, which get byte stores of exactly the tile's own bytes.
-constexpr uint32_t kStageSlots = 4;
-constexpr uint32_t kStageBytes = kThreadsPerBlock * 16;  // one tile of one output
-
-__device__ __forceinline__ void lds_store16(uint32_t addr, const uint4& v) {
-  v4u w;
-  w.x = v.x;
-  w.y = v.y;
-  w.z = v.z;
-  w.w = v.w;
-  *reinterpret_cast<__attribute__((address_space(3))) v4u*>(static_cast<uintptr_t>(addr)) = w;
-}
-__device__ __forceinline__ uint32_t lds_u32_at(uint32_t addr) {
-  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
-      static_cast<uintptr_t>(addr));
-}
-__device__ __forceinline__ uint2 lds_u64_at(uint32_t addr) {
-  const v2u v = *reinterpret_cast<const __attribute__((address_space(3))) v2u*>(
-      static_cast<uintptr_t>(addr));
-  return make_uint2(v.x, v.y);
-}
-
-// 16 bytes at an even LDS byte address (wave-uniform alignment class).
-__device__ __forceinline__ uint4 lds_read16_unaligned(uint32_t addr, uint32_t mis) {
-  if ((mis & 7) == 0) {
-    const uint2 a = lds_u64_at(addr), b = lds_u64_at(addr + 8);
-    return make_uint4(a.x, a.y, b.x, b.y);
+  for (int j = 0; j < K; ++j) {
+    const uint8_t* a = frags + d.in_idx[j] * p.frag_stride;
+    x[j] = *reinterpret_cast<const uint4*>(a);
   }
-  if ((mis & 3) == 0)
-    return make_uint4(lds_u32_at(addr), lds_u32_at(addr + 4), lds_u32_at(addr + 8),
-                      lds_u32_at(addr + 12));
-  // 2 mod 4: five dwords, funnel-shifted by 16 bits
-  const uint32_t a = addr - 2;
-  const uint32_t d0 = lds_u32_at(a), d1 = lds_u32_at(a + 4), d2 = lds_u32_at(a + 8),
-                 d3 = lds_u32_at(a + 12), d4 = lds_u32_at(a + 16);
-  return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, 2), __builtin_amdgcn_alignbyte(d2, d1, 2),
-                    __builtin_amdgcn_alignbyte(d3, d2, 2), __builtin_amdgcn_alignbyte(d4, d3, 2));
 }
 
-// Slot destinations are packed 8 bits each into one register: a private
-// array here would be promoted to static LDS by hipcc, which would move the
-// dynamic LDS base away from address 0 (see launch()).
-struct Stager {
-  uint32_t base;  // LDS byte address of slot 0
-  uint32_t n;     // slots filled
-  uint32_t dest;  // destination fragment of slot q in bits 8q..8q+7
-};
-
-// Write every staged output back, line-aligned, then free the slots.  The
-// tile covers payload bytes [T, T + 4096) of each destination fragment.
-__device__ __forceinline__ void stage_flush(Stager& st, uint8_t* obj, uint32_t bs, uint32_t T) {
-  if (st.n == 0) return;
-  __syncthreads();
-  for (uint32_t q = 0; q < st.n; ++q) {
-    uint8_t* x0 = obj + static_cast<uint64_t>((st.dest >> (8 * q)) & 0xFFu) * bs + T;
-    const uint32_t delta = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(x0) & 127u);
-    uint8_t* a0 = x0 - delta;
-    const uint32_t slot = st.base + q * (kStageBytes + 128);
-    for (uint32_t c = threadIdx.x; c < kThreadsPerBlock + 8; c += kThreadsPerBlock) {
-      const int32_t off = static_cast<int32_t>(16 * c) - static_cast<int32_t>(delta);
-      if (off <= -16 || off >= static_cast<int32_t>(kStageBytes)) continue;
-      const uint4 v = lds_read16_unaligned(slot + 64 + off, delta);
-      if (off >= 0 && off + 16 <= static_cast<int32_t>(kStageBytes)) {
-        st_stream(a0 + 16 * c, v);
-      } else {
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-        for (int i = 0; i < 16; ++i)
-          if (off + i >= 0 && off + i < static_cast<int32_t>(kStageBytes))
-            a0[16 * c + i] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
-      }
-    }
-  }
-  __syncthreads();
-  st.n = 0;
-  st.dest = 0;
-}
-
-__device__ __forceinline__ void stage_put(Stager& st, const uint4& v, uint32_t dest,
-                                          uint8_t* obj, uint32_t bs, uint32_t T) {
-  if (st.n == kStageSlots) stage_flush(st, obj, bs, T);
-  lds_store16(st.base + st.n * (kStageBytes + 128) + 64 + 16 * threadIdx.x, v);
-  st.dest |= dest << (8 * st.n);
-  ++st.n;
-}
-
+// Decode output alignment.  Data fragment j of an object starts at byte
+// j*bs, and bs = 2*ceil(L/2k) leaves it at an arbitrary even offset from a
+// 128-B line, while lanes are aligned to the fragment payloads they read.
+// A wave's 1 KiB store then covers 9 lines, 2 of them partial, and partial
+// nontemporal line writes cost ~20% of the decode (tools/microbench.hip
+// "dstream nt" 450 us vs "dshift nt" 395 us).  Staging in LDS (4 KiB per
+// output per tile, barriers) and in-register 16-B realignment (DPP) were
+// measured slower.  What works: the copies of surviving data fragments are
+// re-read at the object's line phase -- lane chunk t - delta_j, so every
+// wave's 1 KiB of copy stores is line-aligned -- and the re-read hits L2
+// because the first read was a cached load ("mix c shift" 400 us).  Rebuilt
+// rows (on average e*k/(k+m) of the k outputs) keep their natural offsets.
 // One interior decode / reconstruct item with inputs in `cur`; prefetches
 // the workgroup's next item (w + step) into `nxt`.  Items are grid-strided
 // (the chip works on a few objects at a time: better DRAM locality than
 // contiguous per-workgroup ranges, measured 513 -> 479 us at k=10 m=4), so
 // the LDS tables are usually reloaded per item (5 KiB from L2).
-template <int K, int NW, bool STAGE>
+template <int K, int NW>
 __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, uint32_t step,
                                             uint32_t end, uint32_t& cur_table, uint4 (&cur)[K],
                                             uint4 (&nxt)[K]) {
@@ -480,21 +390,12 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
   }
   pin(s);
 
-  if (STAGE && !p.reconstruct) {
-    const uint32_t T = tile * kStageBytes;
-    Stager st{static_cast<uint32_t>(K * kTableBytesPerInput), 0, 0};
-    if (d.copy_inputs) {
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const uint32_t idx = d.in_idx[j];
-        if (idx < K) stage_put(st, cur[j], idx, out, bs, T);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < kRowsPerPass; ++r)
-      if (r < static_cast<int>(n_out)) stage_put(st, row_chunk(s, r), d.out_idx[r], out, bs, T);
-    stage_flush(st, out, bs, T);
-    return;
+  for (int r = 0; r < kRowsPerPass; ++r) {
+    if (r >= static_cast<int>(n_out)) break;
+    uint8_t* dst = p.reconstruct ? out + kHeaderBytes + t
+                                 : out + static_cast<uint64_t>(d.out_idx[r]) * bs + t;
+    st_stream(dst, row_chunk(s, r));
   }
   if (d.copy_inputs) {
 #pragma unroll
@@ -503,22 +404,12 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
       if (idx < K) st_stream(out + static_cast<uint64_t>(idx) * bs + t, cur[j]);
     }
   }
-#pragma unroll
-  for (int r = 0; r < kRowsPerPass; ++r) {
-    if (r >= static_cast<int>(n_out)) break;
-    uint8_t* dst = p.reconstruct ? out + kHeaderBytes + t
-                                 : out + static_cast<uint64_t>(d.out_idx[r]) * bs + t;
-    st_stream(dst, row_chunk(s, r));
-  }
 }
 
-template <int K, int NW, int MINW = 1, bool STRIDE = true, bool STAGE = true>
-__global__ void __launch_bounds__(kThreadsPerBlock, MINW) decode_kernel(DecodeParams p) {
-  const uint32_t items = p.n_obj * p.first_edge;
-  const uint32_t per = (items + gridDim.x - 1) / gridDim.x;
-  const uint32_t begin = STRIDE ? blockIdx.x : blockIdx.x * per;
-  const uint32_t end = STRIDE ? items : min(items, begin + per);
-  const uint32_t step = STRIDE ? gridDim.x : 1;
+template <int K, int NW>
+__global__ void __launch_bounds__(kThreadsPerBlock) decode_kernel(DecodeParams p) {
+  const uint32_t end = p.n_obj * p.first_edge;
+  const uint32_t begin = blockIdx.x, step = gridDim.x;
   uint32_t cur_table = 0xFFFFFFFFu;
   uint4 xa[K], xb[K];
   uint32_t w = begin;
@@ -528,11 +419,70 @@ __global__ void __launch_bounds__(kThreadsPerBlock, MINW) decode_kernel(DecodePa
     decode_load<K>(p, o, t, xa);
   }
   while (w < end) {
-    decode_item<K, NW, STAGE>(p, w, step, end, cur_table, xa, xb);
+    decode_item<K, NW>(p, w, step, end, cur_table, xa, xb);
     w += step;
     if (w >= end) break;
-    decode_item<K, NW, STAGE>(p, w, step, end, cur_table, xb, xa);
+    decode_item<K, NW>(p, w, step, end, cur_table, xb, xa);
     w += step;
+  }
+}
+
+// Interior decode with line-aligned copies (p.copy_shift).  No cross-item
+// prefetch here: the shifted re-reads must follow the aligned reads closely
+// to hit L2 (with a one-item prefetch distance they missed: 544 us).
+template <int K, int NW>
+__global__ void __launch_bounds__(kThreadsPerBlock) decode_shift_kernel(DecodeParams p) {
+  const uint32_t end = p.n_obj * p.first_edge;
+  uint32_t cur_table = 0xFFFFFFFFu;
+  for (uint32_t w = blockIdx.x; w < end; w += gridDim.x) {
+    uint32_t o, tile, t;
+    tile_of(w, p.first_edge, 0, o, tile, t);
+    const ObjDesc& d = p.desc[o];
+    const uint8_t* fb = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes;
+    uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
+    uint4 x[K], c[K];
+    int32_t src[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+      x[j] = *reinterpret_cast<const uint4*>(fb + d.in_idx[j] * p.frag_stride + t);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const uint32_t idx = d.in_idx[j];
+      src[j] = -16;
+      if (idx >= K || !d.copy_inputs) continue;
+      const uint32_t delta = static_cast<uint32_t>(
+          reinterpret_cast<uintptr_t>(out + static_cast<uint64_t>(idx) * p.bs) & 127u);
+      src[j] = static_cast<int32_t>(t) - static_cast<int32_t>(delta);
+      if (src[j] > -16)
+        c[j] = *reinterpret_cast<const uint4*>(fb + idx * p.frag_stride + src[j]);
+    }
+    ensure_tables(p, d, cur_table);
+    const uint32_t n_out = d.n_out;
+    uint2 s[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s[i] = make_uint2(0, 0);
+    if (n_out != 0) {
+#pragma unroll
+      for (int j = 0; j < K; ++j) mac_chunk<NW>(j * kTableBytesPerInput, x[j], s);
+    }
+    pin(s);
+#pragma unroll
+    for (int r = 0; r < kRowsPerPass; ++r) {
+      if (r >= static_cast<int>(n_out)) break;
+      st_stream(out + static_cast<uint64_t>(d.out_idx[r]) * p.bs + t, row_chunk(s, r));
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (src[j] <= -16) continue;  // not a data fragment, or nothing of this chunk is ours
+      uint8_t* dst0 = out + static_cast<uint64_t>(d.in_idx[j]) * p.bs;
+      if (src[j] >= 0) {
+        st_stream(dst0 + src[j], c[j]);
+      } else {  // the fragment's first chunk: only its payload bytes
+        const uint32_t wv[4] = {c[j].x, c[j].y, c[j].z, c[j].w};
+        for (int i = -src[j]; i < 16; ++i)
+          dst0[src[j] + i] = static_cast<uint8_t>(wv[i >> 2] >> (8 * (i & 3)));
+      }
+    }
   }
 }
 
@@ -553,6 +503,19 @@ __global__ void __launch_bounds__(kThreadsPerBlock) decode_edge_kernel(DecodePar
     ensure_tables(p, d, cur_table);
     uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
     if (p.reconstruct && tile == 0) reconstruct_header(p, d, out);
+    if (p.copy_shift && d.copy_inputs && tile == p.first_edge && threadIdx.x < 8) {
+      // the interior's shifted copies stop up to 127 B short of its end
+      const uint32_t te = p.first_edge * kThreadsPerBlock * 16 - 128 + 16 * threadIdx.x;
+      const uint8_t* fb = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + te;
+      for (uint32_t j = 0; j < p.k; ++j) {
+        const uint32_t idx = d.in_idx[j];
+        if (idx >= p.k) continue;
+        const int64_t n = object_bytes(idx, p.bs, te, p.obj_len);
+        if (n > 0)
+          store_partial(out + static_cast<uint64_t>(idx) * p.bs + te,
+                        *reinterpret_cast<const uint4*>(fb + idx * p.frag_stride), n);
+      }
+    }
     if (t >= p.bs) continue;
     const uint8_t* frags =
         p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
@@ -608,11 +571,6 @@ inline void split_tiles(uint32_t bs, uint64_t obj_len, uint32_t k, bool whole_pa
   first_edge = static_cast<uint32_t>(room / (kThreadsPerBlock * 16));
 }
 
-int variant(const char* name) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : 0;
-}
-
 // The kernels address LDS by raw byte offset from 0, which is only valid when
 // the kernel has no static __shared__ data (the dynamic allocation then
 // starts at address 0).  Checked once per kernel; a violation fails loudly.
@@ -639,21 +597,7 @@ template <int K, int NW>
 hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   const size_t lds = K * kTableBytesPerInput;
   split_tiles(p.bs, p.obj_len, K, false, p.tiles, p.first_edge);
-  hipError_t e;
-  if constexpr (K == 10) {
-    // tuning experiment: ECAMD_MINW = minimum waves per SIMD for the main kernel
-    const int minw = variant("ECAMD_MINW");
-    const bool pipe = variant("ECAMD_NOPIPE") == 0;
-    const uint32_t n = p.n_obj * p.first_edge;
-    if (!pipe && minw == 6) e = launch(encode_kernel<K, NW, 6, false>, p, lds, n, stream);
-    else if (!pipe && minw == 5) e = launch(encode_kernel<K, NW, 5, false>, p, lds, n, stream);
-    else if (!pipe) e = launch(encode_kernel<K, NW, 1, false>, p, lds, n, stream);
-    else if (minw == 3) e = launch(encode_kernel<K, NW, 3>, p, lds, n, stream);
-    else if (minw == 4) e = launch(encode_kernel<K, NW, 4>, p, lds, n, stream);
-    else e = launch(encode_kernel<K, NW>, p, lds, n, stream);
-  } else {
-    e = launch(encode_kernel<K, NW>, p, lds, p.n_obj * p.first_edge, stream);
-  }
+  const hipError_t e = launch(encode_kernel<K, NW>, p, lds, p.n_obj * p.first_edge, stream);
   if (e != hipSuccess) return e;
   return launch(encode_edge_kernel<NW>, p, lds, p.n_obj * (p.tiles - p.first_edge), stream);
 }
@@ -661,22 +605,15 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
 template <int K, int NW>
 hipError_t launch_decode_k(DecodeParams p, hipStream_t stream) {
   const size_t lds_tables = K * kTableBytesPerInput;
-  // + output staging slots (decode only), each with 64 B of slack either side
-  const size_t lds = lds_tables + (p.reconstruct ? 0 : kStageSlots * (kStageBytes + 128));
   split_tiles(p.bs, p.obj_len, K, p.reconstruct != 0, p.tiles, p.first_edge);
-  hipError_t e;
-  if constexpr (K == 10) {
-    const int minw = variant("ECAMD_MINW");
-    if (variant("ECAMD_NOSTAGE"))
-      e = launch(decode_kernel<K, NW, 1, true, false>, p, lds, p.n_obj * p.first_edge, stream);
-    else if (variant("ECAMD_DCONTIG"))
-      e = launch(decode_kernel<K, NW, 1, false>, p, lds, p.n_obj * p.first_edge, stream);
-    else if (minw == 3) e = launch(decode_kernel<K, NW, 3>, p, lds, p.n_obj * p.first_edge, stream);
-    else if (minw == 4) e = launch(decode_kernel<K, NW, 4>, p, lds, p.n_obj * p.first_edge, stream);
-    else e = launch(decode_kernel<K, NW>, p, lds, p.n_obj * p.first_edge, stream);
-  } else {
-    e = launch(decode_kernel<K, NW>, p, lds, p.n_obj * p.first_edge, stream);
-  }
+  // Shifted interior copies leave up to 127 B before the interior's end to
+  // the first edge tile, so decode always has one (and first_edge >= 1
+  // keeps its start offset non-negative).
+  if (!p.reconstruct && p.first_edge == p.tiles && p.first_edge > 0) --p.first_edge;
+  p.copy_shift = !p.reconstruct && p.first_edge > 0 && std::getenv("ECAMD_DSHIFT");
+  const uint32_t n = p.n_obj * p.first_edge;
+  const hipError_t e = p.copy_shift ? launch(decode_shift_kernel<K, NW>, p, lds_tables, n, stream)
+                                    : launch(decode_kernel<K, NW>, p, lds_tables, n, stream);
   if (e != hipSuccess) return e;
   return launch(decode_edge_kernel<NW>, p, lds_tables, p.n_obj * (p.tiles - p.first_edge), stream);
 }

@@ -72,6 +72,7 @@ struct DecodeParams {
   uint32_t n_obj;
   uint32_t reconstruct;     // 1 = write fragment payload + header
   uint32_t tiles, first_edge;  // set by the launcher (ec_kernels.hip: split_tiles)
+  uint32_t copy_shift;      // set by the launcher: interior copies are line-aligned
 };
 
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);

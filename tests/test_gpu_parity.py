@@ -95,7 +95,8 @@ def _batch_layout(k, m, n_obj, obj_len):
 
 @pytest.mark.parametrize("k,m,obj_len", [(10, 4, 1 << 20), (10, 4, 4 * 1024 * 1024 // 7),
                                          (4, 2, 100001), (12, 4, 999999), (6, 9, 65538),
-                                         (3, 1, 17)])
+                                         (3, 1, 17), (10, 4, 10 * 4096 * 3),
+                                         (8, 3, 8 * 8192), (10, 4, 10 * 4096 + 2)])
 def test_batch_encode_decode_reconstruct(oracle, gpu, k, m, obj_len):
     import torch
     from pyeclib_amd import batch
@@ -170,7 +171,8 @@ def test_golden_fixtures_on_gpu(amd):
         assert [hashlib.sha256(f).hexdigest() for f in rebuilt] == case["rebuilt_sha256"]
 
 
-@pytest.mark.parametrize("obj_len", [4 * 1024 * 1024, 4194560, 3 * 1024 * 1024 + 22])
+@pytest.mark.parametrize("obj_len", [4 * 1024 * 1024, 4194560, 3 * 1024 * 1024 + 22,
+                                     10 * 4096 * 102])
 def test_batch_full_size_properties(gpu, obj_len):
     """Full-size batch (64 x ~4 MiB, k=10 m=4): size-independent properties
     instead of the oracle -- parity row 0 == XOR of the data fragments, every

@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(256) dstream_kernel(const uint8_t* frags, uint
 // Same pattern with the copy realigned on the load side: each lane loads
 // fragment j at payload offset t - delta_j (unaligned) so that its store to
 // the object lands on a 16-B boundary and every wave writes whole lines.
-template <int K, bool NT>
+template <int K, bool NT, uint32_t MASK = 127>
 __global__ void __launch_bounds__(256) dstream_shift_kernel(const uint8_t* frags, uint8_t* objs,
                                                             uint32_t bs, uint32_t n_obj,
                                                             uint64_t obj_stride, uint64_t fs,
@@ -146,16 +146,120 @@ __global__ void __launch_bounds__(256) dstream_shift_kernel(const uint8_t* frags
     uint4 x[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const uint32_t delta = (j * bs) & 127u;
+      const uint32_t delta = (j * bs) & MASK;
       const uint4* a = reinterpret_cast<const uint4*>(src + j * fs - delta);
       if constexpr (NT) x[j] = ld_stream(a); else x[j] = *a;
     }
     uint8_t* dst = objs + o * obj_stride + t;
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const uint32_t delta = (j * bs) & 127u;
+      const uint32_t delta = (j * bs) & MASK;
       uint4* d = reinterpret_cast<uint4*>(dst + uint64_t(j) * bs - delta);
       if constexpr (NT) st_stream(d, x[j]); else *d = x[j];
+    }
+  }
+}
+
+// Aligned loads; the copy is re-aligned to 16 B in registers: lane L's
+// store chunk takes its low r bytes from lane L-1 (DPP wave_shr:1) and the
+// rest from itself, so every store is a 16-B aligned dwordx4 except one
+// partial chunk at each end of the wave's 1 KiB span.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ uint4 funnel16(const uint4& prev, const uint4& own, uint32_t r) {
+  // bytes [16 - r, 32 - r) of prev||own, r even in [2, 14]
+  const uint32_t w[8] = {prev.x, prev.y, prev.z, prev.w, own.x, own.y, own.z, own.w};
+  const uint32_t q = (16 - r) >> 2, b = (16 - r) & 3;
+  uint32_t o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint32_t lo = w[i], hi = w[i + 1];
+    if (q == 1) { lo = w[i + 1]; hi = w[i + 2]; }
+    if (q == 2) { lo = w[i + 2]; hi = w[i + 3]; }
+    if (q == 3) { lo = w[i + 3]; hi = w[i + 4]; }
+    o[i] = __builtin_amdgcn_alignbyte(hi, lo, b);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+template <int K>
+__global__ void __launch_bounds__(256) dstream_dpp_kernel(const uint8_t* frags, uint8_t* objs,
+                                                          uint32_t bs, uint32_t n_obj,
+                                                          uint64_t obj_stride, uint64_t fs,
+                                                          uint32_t tiles) {
+  const uint32_t items = n_obj * tiles;
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
+    const uint32_t o = w / tiles, tile = w % tiles;
+    const uint32_t t = (tile * 256 + threadIdx.x) * 16;
+    const uint8_t* src = frags + o * (K + 4) * fs + 128 + t;
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = ld_stream(src + j * fs);
+    uint8_t* dst = objs + o * obj_stride + t;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      uint8_t* d = dst + uint64_t(j) * bs;
+      const uint32_t r = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(d) & 15u);
+      if (r == 0) { st_stream(d, x[j]); continue; }
+      const uint4 prev = make_uint4(wave_shr1(x[j].x), wave_shr1(x[j].y), wave_shr1(x[j].z),
+                                    wave_shr1(x[j].w));
+      const uint4 v = funnel16(prev, x[j], r);
+      uint8_t* a = d - r;
+      if (lane != 0) {
+        st_stream(a, v);
+      } else {
+        const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+        for (uint32_t i = r; i < 16; ++i) a[i] = static_cast<uint8_t>(wv[i >> 2] >> (8 * (i & 3)));
+      }
+      if (lane == 63) {
+        const uint32_t wv[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+        for (uint32_t i = 16 - r; i < 16; ++i) a[i + 16] = static_cast<uint8_t>(wv[i >> 2] >> (8 * (i & 3)));
+      }
+    }
+  }
+}
+
+// Decode-shaped mix: K aligned loads (nt or cached), E rebuilt rows (XOR of
+// all inputs) stored at their natural unaligned offsets, K-E copies either
+// stored unaligned from the aligned loads (SHIFT=false) or re-loaded at the
+// object's line phase (cached load, hopefully from L2) and stored aligned.
+template <int K, int E, bool LNT, bool SHIFT>
+__global__ void __launch_bounds__(256) dmix_kernel(const uint8_t* frags, uint8_t* objs,
+                                                   uint32_t bs, uint32_t n_obj,
+                                                   uint64_t obj_stride, uint64_t fs,
+                                                   uint32_t tiles) {
+  const uint32_t items = n_obj * tiles;
+  for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
+    const uint32_t o = w / tiles, tile = w % tiles;
+    const uint32_t t = (tile * 256 + threadIdx.x) * 16;
+    const uint8_t* src = frags + o * (K + 4) * fs + 128 + t;
+    uint4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if constexpr (LNT) x[j] = ld_stream(src + j * fs);
+      else x[j] = *reinterpret_cast<const uint4*>(src + j * fs);
+    }
+    uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      acc.x ^= x[j].x; acc.y ^= x[j].y; acc.z ^= x[j].z; acc.w ^= x[j].w;
+    }
+    uint8_t* dst = objs + o * obj_stride + t;
+#pragma unroll
+    for (int j = 0; j < E; ++j) {
+      acc.x += j;
+      st_stream(dst + uint64_t(j) * bs, acc);
+    }
+#pragma unroll
+    for (int j = E; j < K; ++j) {
+      if constexpr (SHIFT) {
+        const uint32_t delta = (j * bs) & 127u;
+        const uint4 v = *reinterpret_cast<const uint4*>(src + j * fs - delta);
+        st_stream(dst + uint64_t(j) * bs - delta, v);
+      } else {
+        st_stream(dst + uint64_t(j) * bs, x[j]);
+      }
     }
   }
 }
@@ -304,6 +408,26 @@ int main(int argc, char** argv) {
                            bs, n_obj, obj_stride, fsd, tl);
       }, 20);
       std::printf("dshift nt  grid=%d/CU %.1f us %.1f GB/s\n", per_cu, ms * 1e3, db / (ms * 1e-3) / 1e9);
+      ms = time_ms([&] {
+        hipLaunchKernelGGL((dstream_shift_kernel<K, true, 15>), grid, dim3(256), 0, 0, frags, objs,
+                           bs, n_obj, obj_stride, fsd, tl);
+      }, 20);
+      std::printf("dshift16nt grid=%d/CU %.1f us %.1f GB/s\n", per_cu, ms * 1e3, db / (ms * 1e-3) / 1e9);
+      ms = time_ms([&] {
+        hipLaunchKernelGGL((dstream_dpp_kernel<K>), grid, dim3(256), 0, 0, frags, objs,
+                           bs, n_obj, obj_stride, fsd, tl);
+      }, 20);
+      std::printf("ddpp nt    grid=%d/CU %.1f us %.1f GB/s\n", per_cu, ms * 1e3, db / (ms * 1e-3) / 1e9);
+#define MIX(LNT, SH, NAME)                                                                  \
+      ms = time_ms([&] {                                                                    \
+        hipLaunchKernelGGL((dmix_kernel<K, 3, LNT, SH>), grid, dim3(256), 0, 0, frags, objs, \
+                           bs, n_obj, obj_stride, fsd, tl);                                 \
+      }, 20);                                                                               \
+      std::printf(NAME "  grid=%d/CU %.1f us %.1f GB/s\n", per_cu, ms * 1e3, db / (ms * 1e-3) / 1e9);
+      MIX(true, false, "mix nt plain ")
+      MIX(false, false, "mix c  plain ")
+      MIX(true, true, "mix nt shift ")
+      MIX(false, true, "mix c  shift ")
       ms = time_ms([&] {
         hipLaunchKernelGGL((dstream_shift_kernel<K, false>), grid, dim3(256), 0, 0, frags, objs,
                            bs, n_obj, obj_stride, fsd, tl);
