@@ -1,0 +1,41 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench, kernel-trace stats and the
+# two HBM PMC passes (FETCH_SIZE / WRITE_SIZE in separate runs).  Every GPU
+# step has its own time limit and the first failure ends the script.
+#   tools/gpu_round.sh TAG [tests|smoke|bench|prof|pmc ...]   (default: all)
+set -euo pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-tests smoke bench prof pmc}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+export TMPDIR=/tmp
+for s in $STEPS; do
+  echo "== $s $(date +%T)"
+  case $s in
+  tests)
+    (cd $R && timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
+        --timeout-method thread > $O/pytest_gpu.log 2>&1)
+    tail -3 $O/pytest_gpu.log ;;
+  smoke)
+    (cd $R && timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1)
+    tail -1 $O/smoke.log ;;
+  bench)
+    (cd $R && timeout -k 10 400 python3 bench.py --host > $O/bench.json 2> $O/bench.err)
+    cat $O/bench.json ;;
+  prof)
+    (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run \
+      -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.err)
+    cat $O/prof_bench.json
+    find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \; ;;
+  pmc)
+    (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run \
+      -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_fetch.log 2>&1)
+    (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run \
+      -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_write.log 2>&1)
+    python3 $R/tools/pmc_summary.py $O/pmc_fetch $O/pmc_write $O/pmc_summary.json ;;
+  *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "gpu_round $TAG done: $STEPS"
