@@ -1,10 +1,11 @@
-// Launch interface of the gfx950 region kernels (ec_kernels.hip).
+// Launch interface of the gfx950 region kernels (ec_kernels_impl.hpp).
 //
-// All kernels compute outputs[r] = XOR_c M[r][c] * inputs[c] over GF(2^16)
-// on little-endian 16-bit symbols, 16 bytes (8 symbols) per lane per input,
-// with M supplied as nibble lookup tables (gf16.hpp: build_nibble_tables)
-// staged in LDS.  They differ only in where inputs come from and where
-// outputs go:
+// All kernels compute outputs[r] = XOR_c M[r][c] * inputs[c] over the code's
+// field -- GF(2^16) on little-endian 16-bit symbols (liberasurecode_rs_vand)
+// or GF(2^8) on bytes (ISA-L layout: isa_l_rs_vand / isa_l_rs_cauchy) -- 16
+// bytes per lane per input, with M supplied as nibble lookup tables
+// (gf16.hpp / gf8.hpp: build_nibble_tables*) staged in LDS.  They differ
+// only in where inputs come from and where outputs go:
 //   encode      inputs  = k slices of a contiguous object (zero padded past
 //                         obj_len: liberasurecode's prepare_fragments_for_encode)
 //               outputs = m parity payloads (+ optional data fragments)
@@ -23,8 +24,27 @@ namespace ecamd {
 
 constexpr int kHeaderBytes = 80;
 constexpr int kThreadsPerBlock = 256;
-constexpr int kTableBytesPerInput = 512;  // 4 nibble positions x 16 values x u64
-constexpr int kRowsPerPass = 4;           // one u64 table entry carries 4 products
+constexpr int kRowsPerPass = 4;  // one table entry carries the products of 4 rows
+
+// Table bytes per input column: 4 nibble positions x 16 values x u64
+// (GF(2^16)) or 2 nibble positions x 16 values x u32 (GF(2^8)).
+__host__ __device__ constexpr uint32_t table_bytes_per_input(uint32_t w) {
+  return w == 16 ? 512u : 128u;
+}
+
+// Decode keeps two table sets in LDS; a slot is rounded up to 256 B so that
+// its base fits the second byte of an LDS address (ec_kernels_impl.hpp, kb).
+__host__ __device__ constexpr uint32_t table_slot_bytes(uint32_t k, uint32_t w) {
+  return (k * table_bytes_per_input(w) + 255u) & ~255u;
+}
+
+// Decode tuning switches (DecodeParams::flags), read from the environment at
+// each launch so that tools/ab_bench.py can compare them in one process:
+// ECAMD_DEC_PLAIN_STORES=1 / ECAMD_DEC_CACHED_LOADS=1 switch decode's output
+// stores / input loads from nontemporal to the default cache policy.
+// ECAMD_XCD=0 turns off the XCD-contiguous work split (every kernel).
+constexpr uint32_t kFlagPlainStores = 1u;
+constexpr uint32_t kFlagCachedLoads = 2u;
 
 struct EncodeParams {
   const uint8_t* objs;      // object o at objs + o * obj_stride
@@ -34,13 +54,14 @@ struct EncodeParams {
   uint8_t* data;            // optional data fragments (o, j), same strides
   uint64_t frag_stride;
   uint64_t stripe_stride;
-  const uint64_t* tables;   // k * 64 entries for this pass
+  const uint32_t* tables;   // k * table_bytes_per_input(w) bytes for this pass
   const uint8_t* headers;   // (k + m) * 80 precomputed headers, or null
-  uint32_t k, m;
+  uint32_t k, m, w;         // w = field bits (16 or 8)
   uint32_t row0, nrows;     // parity rows handled by this pass
   uint32_t bs;              // payload bytes per fragment
   uint32_t n_obj;
-  uint32_t tiles, first_edge;  // set by the launcher (ec_kernels.hip: split_tiles)
+  uint32_t tiles, first_edge;  // set by the launcher (split_tiles)
+  uint32_t xcd_split;          // set by the launcher (item_range)
 };
 
 // Per-object decode / reconstruct descriptor (device memory).
@@ -51,7 +72,7 @@ struct ObjDesc {
   uint8_t n_out;        // rows in this pass
   uint8_t copy_inputs;  // decode pass 0: copy present data inputs to the object
   uint8_t pad[2];
-  uint32_t table;       // table set index (k * 64 u64 each, per pass)
+  uint32_t table;       // table set index (k * table_bytes_per_input(w) bytes each)
   uint32_t header;      // reconstruct: header row index, else unused
   uint32_t pad2;
 };
@@ -65,18 +86,25 @@ struct DecodeParams {
                             // reconstruct: fragment o at out + o*out_stride
   uint64_t out_stride;
   const ObjDesc* desc;
-  const uint64_t* tables;   // table sets
+  const uint32_t* tables;   // table sets
   const uint8_t* headers;   // reconstruct: header rows (80 B), else null
-  uint32_t k, m;
+  uint32_t k, m, w;
   uint32_t bs;
   uint32_t n_obj;
   uint32_t reconstruct;     // 1 = write fragment payload + header
-  uint32_t tiles, first_edge;  // set by the launcher (ec_kernels.hip: split_tiles)
-  uint32_t copy_shift;      // set by the launcher: interior copies are line-aligned
+  uint32_t tiles, first_edge;  // set by the launcher (split_tiles)
+  uint32_t xcd_split;          // set by the launcher (item_range)
+  uint32_t flags;              // set by the launcher (kFlag*)
 };
 
+// Dispatch on p.w.
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);
 hipError_t launch_decode(const DecodeParams& p, hipStream_t stream);
+// Per-field instantiations (ec_gf16.hip, ec_gf8.hip).
+hipError_t launch_encode_gf16(const EncodeParams& p, hipStream_t stream);
+hipError_t launch_decode_gf16(const DecodeParams& p, hipStream_t stream);
+hipError_t launch_encode_gf8(const EncodeParams& p, hipStream_t stream);
+hipError_t launch_decode_gf8(const DecodeParams& p, hipStream_t stream);
 
 // Number of 256-chunk tiles per fragment payload.
 inline uint32_t tiles_per_fragment(uint32_t bs) {

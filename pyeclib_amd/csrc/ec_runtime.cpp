@@ -407,10 +407,11 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
     P.out = J.out;
     P.out_stride = J.out_stride;
     P.desc = reinterpret_cast<const ObjDesc*>(r->dev.p);
-    P.tables = reinterpret_cast<const uint64_t*>(I.pool.p);
+    P.tables = reinterpret_cast<const uint32_t*>(I.pool.p);
     P.headers = hdr_bytes ? r->dev.b() + desc_bytes : nullptr;
     P.k = k;
     P.m = I.m;
+    P.w = kGfBits;
     P.bs = static_cast<uint32_t>(bs);
     P.n_obj = J.n_obj;
     P.reconstruct = J.dest ? 1 : 0;
@@ -455,10 +456,11 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
     P.data = data;
     P.frag_stride = frag_stride;
     P.stripe_stride = stripe_stride;
-    P.tables = reinterpret_cast<const uint64_t*>(I.enc_tables.b()) + p * I.table_words();
+    P.tables = reinterpret_cast<const uint32_t*>(I.enc_tables.b() + p * I.table_words() * 8);
     P.headers = r ? r->dev.b() : nullptr;
     P.k = k;
     P.m = m;
+    P.w = kGfBits;
     P.row0 = p * kRowsPerPass;
     P.nrows = std::min<uint32_t>(kRowsPerPass, m - P.row0);
     P.bs = static_cast<uint32_t>(bs);

@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""A/B timing of the kernels' tuning switches, interleaved in one process.
+
+Each positional argument is one variant: "base" (no switches) or a
+comma-separated list of VAR=VAL environment settings, e.g.
+    python tools/ab_bench.py base ECAMD_XCD=0 ECAMD_DEC_PLAIN_STORES=1
+The launcher reads the switches at every launch (ec_kernels_impl.hpp), so the
+variants run round-robin in one process on the same buffers (the workload of
+bench.py: k=10 m=4, 256 x 4 MiB, 4 erasures per object).  Every variant's
+decode output is checked against the objects and its parity against the
+first variant's.  Prints median / min microseconds per launch and GB/s of
+algorithmic bytes.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import statistics
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+KEYS = ("ECAMD_XCD", "ECAMD_DEC_PLAIN_STORES", "ECAMD_DEC_CACHED_LOADS")
+
+
+def parse_variant(text):
+    if text == "base":
+        return {}
+    env = {}
+    for part in text.split(","):
+        key, _, val = part.partition("=")
+        env[key] = val
+    return env
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("variants", nargs="+")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--obj-bytes", type=int, default=4 * 1024 * 1024)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--m", type=int, default=4)
+    args = ap.parse_args()
+
+    import torch
+    from pyeclib_amd import batch
+
+    k, m, n, B = args.k, args.m, args.obj_bytes, args.batch
+    dev = torch.device("cuda:0")
+    bs = batch.blocksize(k, n)
+    stride = (n + 255) // 256 * 256
+    gen = torch.Generator(device=dev).manual_seed(20261015)
+    objs = torch.randint(0, 256, (B, stride), dtype=torch.uint8, device=dev, generator=gen)
+    stripes = batch.stripe_buffer(B, k, m, bs, device=dev)
+    codec = batch.BatchCodec(k, m)
+    codec.encode(objs, n, parity=stripes[:, k:], data=stripes[:, :k])
+    ref_parity = stripes[:, k:].clone()
+    rng = np.random.default_rng(7)
+    full = (1 << (k + m)) - 1
+    masks = [full & ~int(sum(1 << int(i) for i in rng.choice(k + m, 4, replace=False)))
+             for _ in range(B)]
+    out = torch.zeros_like(objs)
+    enc_bytes = B * (n + m * (bs + 80))
+    dec_bytes = B * (k * bs + n)
+
+    variants = [(v, parse_variant(v)) for v in args.variants]
+    times = {v: {"enc": [], "dec": []} for v, _ in variants}
+    base_env = {key: os.environ.get(key) for key in KEYS}
+
+    def apply(env):
+        for key in KEYS:
+            if base_env[key] is None:
+                os.environ.pop(key, None)
+            else:
+                os.environ[key] = base_env[key]
+        os.environ.update(env)
+
+    for rnd in range(args.rounds):
+        for name, env in variants:
+            apply(env)
+            codec.encode(objs, n, parity=stripes[:, k:])
+            codec.decode(stripes, n, masks, out)
+            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            torch.cuda.synchronize()
+            ev[0].record()
+            for _ in range(args.reps):
+                codec.encode(objs, n, parity=stripes[:, k:])
+            ev[1].record()
+            for _ in range(args.reps):
+                codec.decode(stripes, n, masks, out)
+            ev[2].record()
+            torch.cuda.synchronize()
+            times[name]["enc"].append(ev[0].elapsed_time(ev[1]) / args.reps * 1e3)
+            times[name]["dec"].append(ev[1].elapsed_time(ev[2]) / args.reps * 1e3)
+            if rnd == 0:
+                assert torch.equal(stripes[:, k:], ref_parity), f"{name}: parity differs"
+                assert torch.equal(out[:, :n], objs[:, :n]), f"{name}: decode differs"
+                out.zero_()
+    apply({})
+
+    print(f"k={k} m={m} {B} x {n} B, {args.rounds} rounds x {args.reps} launches")
+    print(f"{'variant':<48} {'enc med us':>10} {'min':>8} {'GB/s':>8} "
+          f"{'dec med us':>10} {'min':>8} {'GB/s':>8}")
+    for name, _ in variants:
+        e, d = times[name]["enc"], times[name]["dec"]
+        em, dm = statistics.median(e), statistics.median(d)
+        print(f"{name:<48} {em:10.1f} {min(e):8.1f} {enc_bytes / em / 1e3:8.1f} "
+              f"{dm:10.1f} {min(d):8.1f} {dec_bytes / dm / 1e3:8.1f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -2,7 +2,7 @@
 # One GPU-box session: parity tests, smoke, bench, kernel-trace stats and the
 # two HBM PMC passes (FETCH_SIZE / WRITE_SIZE in separate runs).  Every GPU
 # step has its own time limit and the first failure ends the script.
-#   tools/gpu_round.sh TAG [tests|smoke|bench|prof|pmc ...]   (default: all)
+#   tools/gpu_round.sh TAG [tests|smoke|ab|bench|prof|pmc ...]   (default: all but ab)
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 TAG=${1:-r01}
@@ -21,6 +21,11 @@ for s in $STEPS; do
   smoke)
     (cd $R && timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1)
     tail -1 $O/smoke.log ;;
+  ab)
+    (cd $R && timeout -k 10 400 python3 tools/ab_bench.py base ECAMD_XCD=0 ECAMD_DEC_PLAIN_STORES=1 \
+        ECAMD_DEC_CACHED_LOADS=1 ECAMD_DEC_PLAIN_STORES=1,ECAMD_DEC_CACHED_LOADS=1 \
+        ECAMD_XCD=0,ECAMD_DEC_PLAIN_STORES=1 > $O/ab.txt 2>&1)
+    cat $O/ab.txt ;;
   bench)
     (cd $R && timeout -k 10 400 python3 bench.py --host > $O/bench.json 2> $O/bench.err)
     cat $O/bench.json ;;
