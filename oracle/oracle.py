@@ -17,6 +17,7 @@ import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _SO = os.path.join(_HERE, "build", "liboracle_rs_vand.so")
+_SO8 = os.path.join(_HERE, "build", "liboracle_isal.so")
 
 HDR = 80
 LIBEC_VERSION = 0x010800
@@ -24,6 +25,11 @@ CHKSUM_NONE = 1
 CHKSUM_CRC32 = 2
 
 _lib = None
+_lib8 = None
+
+# GF(2^8) ISA-L codes (isal_oracle.c): backend ids of the two matrix kinds
+ISAL_VAND = 4
+ISAL_CAUCHY = 7
 
 
 def build() -> str:
@@ -139,3 +145,76 @@ def encode_payloads_into(k: int, m: int, data_ptr: int, length: int, out_ptr: in
                           ctypes.c_void_p(out_ptr))
     if rc != 0:
         raise RuntimeError(f"orc_encode rc={rc}")
+
+
+# ---------------- GF(2^8) ISA-L codes (isal_oracle.c) ----------------
+
+def lib8() -> ctypes.CDLL:
+    global _lib8
+    if _lib8 is None:
+        if not os.path.exists(_SO8):
+            build()
+        L = ctypes.CDLL(_SO8)
+        u8p = ctypes.c_void_p
+        L.o8_blocksize.argtypes = [ctypes.c_int, ctypes.c_uint64]
+        L.o8_blocksize.restype = ctypes.c_uint64
+        L.o8_generator.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, u8p]
+        L.o8_gf_mul.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.o8_encode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_uint32, u8p, ctypes.c_uint64, u8p]
+        L.o8_decode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, u8p,
+                                ctypes.POINTER(ctypes.c_uint64)]
+        L.o8_reconstruct.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_uint32, ctypes.POINTER(ctypes.c_char_p),
+                                     ctypes.c_int, ctypes.c_uint64, ctypes.c_int, u8p]
+        _lib8 = L
+    return _lib8
+
+
+def isal_blocksize(k: int, length: int) -> int:
+    return lib8().o8_blocksize(k, length)
+
+
+def isal_generator(kind: int, k: int, m: int) -> list[list[int]]:
+    buf = ctypes.create_string_buffer((k + m) * k)
+    assert lib8().o8_generator(kind, k, m, buf) == 0
+    raw = buf.raw
+    return [list(raw[r * k:(r + 1) * k]) for r in range(k + m)]
+
+
+def isal_gf_mul(a: int, b: int) -> int:
+    return lib8().o8_gf_mul(a, b)
+
+
+def isal_encode(kind: int, k: int, m: int, data: bytes, ct: int = CHKSUM_NONE,
+                libec_version: int = LIBEC_VERSION) -> list[bytes]:
+    fl = isal_blocksize(k, len(data)) + HDR
+    out = ctypes.create_string_buffer(fl * (k + m))
+    rc = lib8().o8_encode(kind, k, m, ct, libec_version, data, len(data), out)
+    if rc != 0:
+        raise RuntimeError(f"o8_encode rc={rc}")
+    raw = out.raw
+    return [raw[i * fl:(i + 1) * fl] for i in range(k + m)]
+
+
+def isal_decode(kind: int, k: int, m: int, frags: list[bytes]) -> bytes:
+    arr = (ctypes.c_char_p * len(frags))(*frags)
+    orig = int.from_bytes(frags[0][12:20], "little")
+    out = ctypes.create_string_buffer(max(orig, 1))
+    olen = ctypes.c_uint64(0)
+    rc = lib8().o8_decode(kind, k, m, arr, len(frags), out, ctypes.byref(olen))
+    if rc != 0:
+        raise RuntimeError(f"o8_decode rc={rc}")
+    return out.raw[:olen.value]
+
+
+def isal_reconstruct(kind: int, k: int, m: int, frags: list[bytes], dest: int,
+                     ct: int = CHKSUM_NONE, libec_version: int = LIBEC_VERSION) -> bytes:
+    fl = len(frags[0])
+    arr = (ctypes.c_char_p * len(frags))(*frags)
+    out = ctypes.create_string_buffer(fl)
+    rc = lib8().o8_reconstruct(kind, k, m, ct, libec_version, arr, len(frags), fl, dest, out)
+    if rc != 0:
+        raise RuntimeError(f"o8_reconstruct rc={rc}")
+    return out.raw

@@ -11,6 +11,11 @@ It shares no code and no algorithm choices with rs_vand_oracle.c:
     reaches the same unique matrix by column operations);
   * region products are vectorised over little-endian uint16 symbol arrays.
 
+The GF(2^8) half restates the ISA-L matrices (isa_l_rs_vand /
+isa_l_rs_cauchy) the same way -- carry-less products modulo 0x11D, Cauchy
+entries as x^254 (the multiplicative inverse), no shared tables -- to check
+oracle/isal_oracle.c.
+
 Only tests/ may import it.
 """
 from __future__ import annotations
@@ -119,3 +124,68 @@ def encode_payloads(k: int, m: int, data: bytes) -> list[bytes]:
     g = generator(k, m)
     par = [region_dot(syms, g[k + r]) for r in range(m)]
     return [s.tobytes() for s in syms] + [p.astype("<u2").tobytes() for p in par]
+
+
+# ---------------- GF(2^8), ISA-L layout ----------------
+
+POLY8 = 0x11D
+
+
+def gf8_mul(a: int, b: int) -> int:
+    r = 0
+    while b:
+        if b & 1:
+            r ^= a
+        b >>= 1
+        a <<= 1
+        if a & 0x100:
+            a ^= POLY8
+    return r
+
+
+def gf8_inv(a: int) -> int:
+    r, base, e = 1, a, 254  # a^(2^8 - 2)
+    while e:
+        if e & 1:
+            r = gf8_mul(r, base)
+        base = gf8_mul(base, base)
+        e >>= 1
+    return r
+
+
+def isal_generator(kind: str, k: int, m: int) -> list[list[int]]:
+    """kind 'vand': rows k.. are 2^((i-k) j); 'cauchy': 1 / (i ^ j)."""
+    rows = [[int(i == j) for j in range(k)] for i in range(k)]
+    for i in range(k, k + m):
+        if kind == "cauchy":
+            rows.append([gf8_inv(i ^ j) for j in range(k)])
+        else:
+            g = 1
+            for _ in range(i - k):
+                g = gf8_mul(g, 2)
+            row, p = [], 1
+            for _ in range(k):
+                row.append(p)
+                p = gf8_mul(p, g)
+            rows.append(row)
+    return rows
+
+
+def _mul_table8(c: int) -> np.ndarray:
+    return np.array([gf8_mul(c, x) for x in range(256)], dtype=np.uint8)
+
+
+def isal_encode_payloads(kind: str, k: int, m: int, data: bytes) -> list[bytes]:
+    bs = (len(data) + k - 1) // k
+    buf = np.zeros(k * bs, dtype=np.uint8)
+    buf[: len(data)] = np.frombuffer(data, dtype=np.uint8)
+    slices = [buf[j * bs:(j + 1) * bs] for j in range(k)]
+    g = isal_generator(kind, k, m)
+    out = [s.tobytes() for s in slices]
+    for r in range(m):
+        acc = np.zeros(bs, dtype=np.uint8)
+        for s, c in zip(slices, g[k + r]):
+            if c:
+                acc ^= _mul_table8(c)[s]
+        out.append(acc.tobytes())
+    return out

@@ -16,9 +16,11 @@ from . import _native
 HEADER = _native.HEADER_SIZE
 
 
-def blocksize(k: int, obj_len: int) -> int:
-    """Payload bytes per fragment: ceil(obj_len / 2k) * 2 (w = 16 alignment)."""
-    mult = 2 * k
+def blocksize(k: int, obj_len: int, w: int = 16) -> int:
+    """Payload bytes per fragment: the object padded to a multiple of
+    k * w/8 bytes, split k ways (liberasurecode get_aligned_data_size; w = 16
+    for rs_vand, 8 for the ISA-L codes)."""
+    mult = k * (w // 8)
     return (obj_len + mult - 1) // mult * mult // k
 
 
@@ -63,12 +65,24 @@ def _stream(stream: Any) -> int | None:
     return int(getattr(stream, "cuda_stream", stream))
 
 
-class BatchCodec:
-    """One (k, m) rs_vand instance driving the batch kernels."""
+# ec_type -> (backend id, field bits)
+_CODES = {"amd_rs_vand": (11, 16), "liberasurecode_rs_vand": (6, 16),
+          "isa_l_rs_vand": (4, 8), "isa_l_rs_cauchy": (7, 8)}
 
-    def __init__(self, k: int, m: int, inline_crc32: bool = False):
-        self.k, self.m = k, m
-        self.handle = _native.init(k, m, 11, m, 1 if inline_crc32 else 0, 0, 0, 0)
+
+class BatchCodec:
+    """One (k, m) instance of a GPU ec_type driving the batch kernels."""
+
+    def __init__(self, k: int, m: int, inline_crc32: bool = False,
+                 ec_type: str = "amd_rs_vand"):
+        if ec_type not in _CODES:
+            raise ValueError(f"{ec_type} has no GPU batch path")
+        backend, self.w = _CODES[ec_type]
+        self.k, self.m, self.ec_type = k, m, ec_type
+        self.handle = _native.init(k, m, backend, m, 1 if inline_crc32 else 0, 0, 0, 0)
+
+    def blocksize(self, obj_len: int) -> int:
+        return blocksize(self.k, obj_len, self.w)
 
     def _check(self, ret: int, fn: str) -> None:
         if ret < 0:

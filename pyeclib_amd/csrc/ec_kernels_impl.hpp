@@ -320,46 +320,44 @@ __device__ __forceinline__ void encode_load(const EncodeParams& p, uint32_t o, u
   for (int j = 0; j < K; ++j) x[j] = ld_stream(obj + static_cast<uint64_t>(j) * p.bs);
 }
 
-// One interior item with its inputs already in `cur`; first issues the loads
-// of the block's next item into `nxt`, so they are in flight while this
-// item's table lookups run.
-template <class F, int K>
-__device__ __forceinline__ void encode_item(const EncodeParams& p, uint32_t w, const ItemRange& r,
+// One interior item with its inputs in `cur`.  PREFETCH: first issue the
+// loads of the block's next item (w + step) into `nxt`, so they are in flight
+// while this item's table lookups run.
+//
+// Every memory operation in here is unconditional (NR output rows, no
+// headers, no data copies) so that hipcc's s_waitcnt insertion sees one
+// sequence per item: before using cur[j] it then waits only for cur's own
+// loads (vmcnt = the ops issued after them), not for the prefetch.  A branch
+// around any load or store in the loop body makes it fall back to the
+// shortest path's count -- measured as vmcnt(9) before cur[0], i.e. waiting
+// for the next item's loads too, which serialised memory and compute.
+template <class F, int K, int NR, bool PREFETCH>
+__device__ __forceinline__ void encode_item(const EncodeParams& p, uint32_t w, uint32_t step,
                                             uint4 (&cur)[K], uint4 (&nxt)[K]) {
   uint32_t o, tile, t;
   tile_of(w, p.first_edge, 0, o, tile, t);
-  if (w + r.step < r.end) {
+  if constexpr (PREFETCH) {
     uint32_t on, tn, ttn;
-    tile_of(w + r.step, p.first_edge, 0, on, tn, ttn);
+    tile_of(w + step, p.first_edge, 0, on, tn, ttn);
     encode_load<K>(p, on, ttn, nxt);
   }
-  if (tile == 0) encode_headers(p, o, K);
   typename F::Acc s;
   F::zero(s);
 #pragma unroll
   for (int j = 0; j < K; ++j) F::mac(F::kb(0), j * F::kTableBytes, cur[j], s);
   F::pin(s);
-
   uint8_t* par = p.parity + static_cast<uint64_t>(o) * p.stripe_stride + p.row0 * p.frag_stride +
                  kHeaderBytes + t;
 #pragma unroll
-  for (int q = 0; q < kRowsPerPass; ++q)
-    if (q < static_cast<int>(p.nrows)) st_stream(par + q * p.frag_stride, F::row(s, q));
-
-  if (p.data != nullptr && p.row0 == 0) {
-    uint8_t* dat = p.data + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
-#pragma unroll
-    for (int j = 0; j < K; ++j) st_stream(dat + j * p.frag_stride, cur[j]);
-  }
+  for (int q = 0; q < NR; ++q) st_stream(par + q * p.frag_stride, F::row(s, q));
 }
 
 // Edge item: payload tail (t + 16 > bs) and chunks reaching the zero padding
 // past obj_len (liberasurecode's prepare_fragments_for_encode zero-fills).
-template <class F, int K>
+template <class F, int K, int NR>
 __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t e) {
   uint32_t o, tile, t;
   tile_of(e, p.tiles - p.first_edge, p.first_edge, o, tile, t);
-  if (tile == 0) encode_headers(p, o, K);
   if (t >= p.bs) return;
   const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride;
   const int64_t rem = static_cast<int64_t>(p.bs) - t;
@@ -373,17 +371,15 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
   F::pin(s);
   uint8_t* par = p.parity + static_cast<uint64_t>(o) * p.stripe_stride + p.row0 * p.frag_stride +
                  kHeaderBytes + t;
-  for (uint32_t q = 0; q < p.nrows; ++q) store_partial(par + q * p.frag_stride, F::row(s, q), rem);
-  if (p.data != nullptr && p.row0 == 0) {
-    uint8_t* dat = p.data + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
 #pragma unroll
-    for (int j = 0; j < K; ++j) store_partial(dat + j * p.frag_stride, x[j], rem);
-  }
+  for (int q = 0; q < NR; ++q) store_partial(par + q * p.frag_stride, F::row(s, q), rem);
 }
 
-template <class F, int K>
+template <class F, int K, int NR>
 __global__ void __launch_bounds__(kThreadsPerBlock) encode_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
+  if (p.headers != nullptr)
+    for (uint32_t o = blockIdx.x; o < p.n_obj; o += gridDim.x) encode_headers(p, o, K);
   __syncthreads();
   const ItemRange r = item_range(p.n_obj * p.first_edge, p.xcd_split);
   uint4 xa[K], xb[K];
@@ -392,16 +388,45 @@ __global__ void __launch_bounds__(kThreadsPerBlock) encode_kernel(EncodeParams p
     uint32_t o, tile, t;
     tile_of(w, p.first_edge, 0, o, tile, t);
     encode_load<K>(p, o, t, xa);
+    // two items per trip so cur / nxt stay compile-time register arrays;
+    // the last item of the range runs without a prefetch
+    while (true) {
+      if (w + r.step >= r.end) {
+        encode_item<F, K, NR, false>(p, w, r.step, xa, xb);
+        break;
+      }
+      encode_item<F, K, NR, true>(p, w, r.step, xa, xb);
+      w += r.step;
+      if (w + r.step >= r.end) {
+        encode_item<F, K, NR, false>(p, w, r.step, xb, xa);
+        break;
+      }
+      encode_item<F, K, NR, true>(p, w, r.step, xb, xa);
+      w += r.step;
+    }
   }
-  // edge items while the first interior loads are in flight
+  // edge items last, on the highest-numbered blocks (those with the fewest
+  // interior items)
   const uint32_t n_edge = p.n_obj * (p.tiles - p.first_edge);
-  for (uint32_t e = blockIdx.x; e < n_edge; e += gridDim.x) encode_edge_item<F, K>(p, e);
-  while (w < r.end) {
-    encode_item<F, K>(p, w, r, xa, xb);
-    w += r.step;
-    if (w >= r.end) break;
-    encode_item<F, K>(p, w, r, xb, xa);
-    w += r.step;
+  for (uint32_t e = gridDim.x - 1 - blockIdx.x; e < n_edge; e += gridDim.x)
+    encode_edge_item<F, K, NR>(p, e);
+}
+
+// Data fragments (optional output of encode): the k padded object slices
+// copied into their fragment payloads.  Item = (object, fragment, 4 KiB tile).
+__global__ void __launch_bounds__(kThreadsPerBlock) copy_data_kernel(EncodeParams p) {
+  const uint32_t per_obj = p.k * p.tiles;
+  const uint32_t items = p.n_obj * per_obj;
+  for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
+    const uint32_t o = w / per_obj, rest = w - o * per_obj;
+    const uint32_t j = rest / p.tiles, tile = rest - j * p.tiles;
+    const uint32_t t = (tile * kThreadsPerBlock + threadIdx.x) << 4;
+    if (t >= p.bs) continue;
+    const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride;
+    const uint4 x = load_clamped(obj, static_cast<uint64_t>(j) * p.bs + t, p.obj_len);
+    store_partial(p.data + static_cast<uint64_t>(o) * p.stripe_stride + j * p.frag_stride +
+                      kHeaderBytes + t,
+                  x, static_cast<int64_t>(p.bs) - t);
   }
 }
 
@@ -690,12 +715,31 @@ hipError_t launch(Kern kern, Params p, size_t lds, uint32_t items, hipStream_t s
   return hipGetLastError();
 }
 
-template <class F, int K>
+template <class F, int K, int NR>
 hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   split_tiles(p.bs, p.obj_len, K, false, p.tiles, p.first_edge);
   const uint32_t interior = p.n_obj * p.first_edge;
   const uint32_t edge = p.n_obj * (p.tiles - p.first_edge);
-  return launch(encode_kernel<F, K>, p, K * F::kTableBytes, std::max(interior, edge), stream);
+  hipError_t e = launch(encode_kernel<F, K, NR>, p, K * F::kTableBytes,
+                        std::max(std::max(interior, edge), p.headers ? p.n_obj : 0u), stream);
+  if (e != hipSuccess || p.data == nullptr || p.row0 != 0) return e;
+  return launch(copy_data_kernel, p, 0, p.n_obj * K * p.tiles, stream);
+}
+
+template <class F, int K>
+hipError_t launch_encode_rows(const EncodeParams& p, hipStream_t stream) {
+  switch (p.nrows) {
+    case 1:
+      return launch_encode_k<F, K, 1>(p, stream);
+    case 2:
+      return launch_encode_k<F, K, 2>(p, stream);
+    case 3:
+      return launch_encode_k<F, K, 3>(p, stream);
+    case 4:
+      return launch_encode_k<F, K, 4>(p, stream);
+    default:
+      return hipErrorInvalidValue;
+  }
 }
 
 template <class F, int K>

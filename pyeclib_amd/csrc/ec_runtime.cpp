@@ -28,13 +28,41 @@
 #include "ec_kernels.hpp"
 #include "erasurecode_amd.h"
 #include "gf16.hpp"
+#include "gf8.hpp"
 
 namespace ecamd {
 namespace {
 
-constexpr uint32_t kLibecVersion = 0x010800;          // fragment format written (1.8.0)
-constexpr uint32_t kRsVandBackendVersion = 0x00010000;  // rs_vand backend 1.0.0
-constexpr uint8_t kWireBackendId = EC_BACKEND_LIBERASURECODE_RS_VAND;
+constexpr uint32_t kLibecVersion = 0x010800;  // fragment format written (1.8.0)
+
+// What a backend id means here: the id written into fragment headers, the
+// backend version stamped next to it ((major << 16) | (minor << 8) | rev, as
+// liberasurecode's backends declare it) and the field width.  amd_rs_vand (11)
+// writes liberasurecode_rs_vand's bytes, id 6 included, so the two ec_types
+// read each other's fragments.  The ISA-L versions are UNPINNED (ISA-L's
+// liberasurecode backends are not in this container; DESIGN.md, Oracle).
+struct Code {
+  uint8_t wire_id;
+  uint32_t version;
+  int w;
+};
+constexpr Code kRsVand{EC_BACKEND_LIBERASURECODE_RS_VAND, 0x00010000, 16};  // rs_vand 1.0.0
+constexpr Code kIsalVand{EC_BACKEND_ISA_L_RS_VAND, 0x00020D00, 8};          // isa_l_rs_vand 2.13.0
+constexpr Code kIsalCauchy{EC_BACKEND_ISA_L_RS_CAUCHY, 0x00020E01, 8};      // isa_l_rs_cauchy 2.14.1
+
+const Code* code_of(int backend_id) {
+  switch (backend_id) {
+    case EC_BACKEND_LIBERASURECODE_RS_VAND:
+    case EC_BACKEND_AMD_RS_VAND:
+      return &kRsVand;
+    case EC_BACKEND_ISA_L_RS_VAND:
+      return &kIsalVand;
+    case EC_BACKEND_ISA_L_RS_CAUCHY:
+      return &kIsalCauchy;
+    default:
+      return nullptr;
+  }
+}
 constexpr int kRing = 4;
 
 inline uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
@@ -64,7 +92,7 @@ uint32_t hdr_crc(const void* p, size_t n, bool legacy) {
 }
 
 // add_fragment_metadata (upstream erasurecode_helpers.c), header into h[0..80)
-void make_header(uint8_t* h, uint32_t idx, uint32_t bs, uint64_t orig, int ct,
+void make_header(uint8_t* h, const Code& code, uint32_t idx, uint32_t bs, uint64_t orig, int ct,
                  const uint8_t* payload, bool legacy) {
   std::memset(h, 0, kHeaderBytes);
   put32(h + 0, idx);
@@ -74,8 +102,8 @@ void make_header(uint8_t* h, uint32_t idx, uint32_t bs, uint64_t orig, int ct,
   h[20] = static_cast<uint8_t>(ct);
   if (ct == CHKSUM_CRC32) put32(h + 21, hdr_crc(payload, bs, legacy));
   h[53] = 0;
-  h[54] = kWireBackendId;
-  put32(h + 55, kRsVandBackendVersion);
+  h[54] = code.wire_id;
+  put32(h + 55, code.version);
   put32(h + 59, LIBERASURECODE_FRAG_HEADER_MAGIC);
   put32(h + 63, kLibecVersion);
   put32(h + 67, hdr_crc(h, sizeof(fragment_metadata_t), legacy));
@@ -136,6 +164,7 @@ struct RingSlot {
 
 struct Instance {
   int k = 0, m = 0, ct = CHKSUM_NONE, backend_id = 0, device = 0;
+  Code code = kRsVand;
   bool legacy_crc = false;
   uint32_t passes = 1;  // ceil(m / 4) table sets per decode pattern
   GfMatrix gen;
@@ -151,7 +180,8 @@ struct Instance {
   hipStream_t hstream[2] = {nullptr, nullptr};  // host-resident pipeline
   DevBuf hbuf[2];
 
-  size_t table_words() const { return static_cast<size_t>(k) * 64; }
+  // bytes of one table set (k inputs x up to 4 rows)
+  size_t table_bytes() const { return static_cast<size_t>(k) * table_bytes_per_input(code.w); }
 
   ~Instance() {
     DeviceGuard g(device);
@@ -236,21 +266,39 @@ int gpu_available() {
   return avail;
 }
 
-uint64_t blocksize_of(int k, uint64_t len) {
-  const uint64_t mult = static_cast<uint64_t>(k) * 2;  // k * w/8, w = 16
+// get_aligned_data_size (upstream erasurecode_helpers.c): the object is padded
+// to a multiple of k * w/8 bytes and split into k equal payloads.
+uint64_t blocksize_of(int k, int w, uint64_t len) {
+  const uint64_t mult = static_cast<uint64_t>(k) * (w / 8);
   return ((len + mult - 1) / mult) * mult / k;
+}
+
+uint16_t gf_mul(int w, uint16_t a, uint16_t b) {
+  return w == 16 ? Gf16::get().mul(a, b) : Gf8::get().mul(a, b);
+}
+
+bool gf_invert(int w, const GfMatrix& a, GfMatrix& out, int n) {
+  return w == 16 ? invert(a, out, n) : invert8(a, out, n);
+}
+
+// Table set(s) for `nrows` rows of a k-column coefficient matrix, in the
+// kernel's layout for the field (one set per 4 rows).
+void build_tables(int w, const uint16_t* rows, int nrows, int k, uint8_t* out) {
+  if (w == 16)
+    build_nibble_tables(rows, nrows, k, reinterpret_cast<uint64_t*>(out));
+  else
+    build_nibble_tables8(rows, nrows, k, reinterpret_cast<uint32_t*>(out));
 }
 
 // Rows of a decode (dest < 0) or reconstruct (dest >= 0) matrix over the
 // inputs `avail` (first k available fragment indices, ascending).
 bool pattern_rows(const Instance& I, const int* avail, int dest, std::vector<uint16_t>& rows,
                   std::vector<int>& out_idx) {
-  const Gf16& gf = Gf16::get();
-  const int k = I.k;
+  const int k = I.k, w = I.code.w;
   GfMatrix sub(static_cast<size_t>(k) * k), inv;
   for (int i = 0; i < k; ++i)
     std::memcpy(&sub[i * k], &I.gen[avail[i] * k], sizeof(uint16_t) * k);
-  if (!invert(sub, inv, k)) return false;
+  if (!gf_invert(w, sub, inv, k)) return false;
   rows.clear();
   out_idx.clear();
   if (dest < 0) {
@@ -269,7 +317,7 @@ bool pattern_rows(const Instance& I, const int* avail, int dest, std::vector<uin
     rows.assign(k, 0);
     for (int c = 0; c < k; ++c) {
       uint16_t acc = 0;
-      for (int j = 0; j < k; ++j) acc ^= gf.mul(I.gen[dest * k + j], inv[j * k + c]);
+      for (int j = 0; j < k; ++j) acc ^= gf_mul(w, I.gen[dest * k + j], inv[j * k + c]);
       rows[c] = acc;
     }
     out_idx.push_back(dest);
@@ -299,9 +347,9 @@ int pool_slot(Instance& I, uint32_t avail_mask, const int* avail, int dest, uint
     return 0;
   }
   if (!pattern_rows(I, avail, dest, rows, out_idx)) return -EINSUFFFRAGS;
-  const size_t words = I.table_words();
+  const size_t set_bytes = I.table_bytes();
   if (I.pool_slots == 0) {
-    const size_t slot_bytes = words * 8 * I.passes;
+    const size_t slot_bytes = set_bytes * I.passes;
     I.pool_slots = static_cast<uint32_t>(std::max<size_t>(64, (size_t(32) << 20) / slot_bytes));
     hipError_t e = I.pool.ensure(slot_bytes * I.pool_slots);
     if (e != hipSuccess) {
@@ -316,16 +364,16 @@ int pool_slot(Instance& I, uint32_t avail_mask, const int* avail, int dest, uint
     I.pool_used = 0;
   }
   const uint32_t s = I.pool_used++;
-  std::vector<uint64_t> host(words * I.passes, 0);
+  std::vector<uint8_t> host(set_bytes * I.passes, 0);
   const int nrows = static_cast<int>(out_idx.size());
   for (uint32_t p = 0; p * kRowsPerPass < static_cast<uint32_t>(nrows); ++p) {
     const int r0 = p * kRowsPerPass;
     const int nr = std::min(kRowsPerPass, nrows - r0);
-    build_nibble_tables(&rows[static_cast<size_t>(r0) * I.k], nr, I.k, &host[p * words]);
+    build_tables(I.code.w, &rows[static_cast<size_t>(r0) * I.k], nr, I.k, &host[p * set_bytes]);
   }
   // The slot is unused by any in-flight kernel, so a synchronous upload is safe.
-  hipError_t e = hipMemcpy(I.pool.b() + static_cast<size_t>(s) * words * 8 * I.passes,
-                           host.data(), host.size() * 8, hipMemcpyHostToDevice);
+  hipError_t e = hipMemcpy(I.pool.b() + static_cast<size_t>(s) * set_bytes * I.passes,
+                           host.data(), host.size(), hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_errno(e);
   I.pool_index.emplace(key, s);
   *slot = s;
@@ -354,7 +402,7 @@ struct DecodeJob {
 // Shared decode / reconstruct launcher (caller holds I.mu, device set).
 int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
   const int k = I.k, n = I.k + I.m;
-  const uint64_t bs = blocksize_of(k, J.obj_len);
+  const uint64_t bs = blocksize_of(k, I.code.w, J.obj_len);
   if (bs == 0) return 0;
   if (J.frag_stride % 16 || J.frag_stride < kHeaderBytes + round16(bs)) return -EINVALIDPARAMS;
   if (J.stripe_stride % 16 || reinterpret_cast<uintptr_t>(J.frags) % 16) return -EINVALIDPARAMS;
@@ -411,7 +459,7 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
     P.headers = hdr_bytes ? r->dev.b() + desc_bytes : nullptr;
     P.k = k;
     P.m = I.m;
-    P.w = kGfBits;
+    P.w = static_cast<uint32_t>(I.code.w);
     P.bs = static_cast<uint32_t>(bs);
     P.n_obj = J.n_obj;
     P.reconstruct = J.dest ? 1 : 0;
@@ -427,7 +475,7 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
                uint8_t* parity, uint8_t* data, uint64_t frag_stride, uint64_t stripe_stride,
                bool headers, hipStream_t stream) {
   const int k = I.k, m = I.m;
-  const uint64_t bs = blocksize_of(k, obj_len);
+  const uint64_t bs = blocksize_of(k, I.code.w, obj_len);
   if (bs == 0 && !headers) return 0;
   if (frag_stride % 16 || frag_stride < kHeaderBytes + round16(bs)) return -EINVALIDPARAMS;
   if (stripe_stride % 16) return -EINVALIDPARAMS;
@@ -443,7 +491,7 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
     r = I.ring_acquire(hdr_bytes, &e);
     if (!r) return hip_errno(e);
     for (int i = 0; i < k + m; ++i)
-      make_header(r->host + i * kHeaderBytes, i, static_cast<uint32_t>(bs), obj_len, I.ct,
+      make_header(r->host + i * kHeaderBytes, I.code, i, static_cast<uint32_t>(bs), obj_len, I.ct,
                   nullptr, I.legacy_crc);
     if ((e = I.ring_commit(r, hdr_bytes, stream)) != hipSuccess) return hip_errno(e);
   }
@@ -456,11 +504,11 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
     P.data = data;
     P.frag_stride = frag_stride;
     P.stripe_stride = stripe_stride;
-    P.tables = reinterpret_cast<const uint32_t*>(I.enc_tables.b() + p * I.table_words() * 8);
+    P.tables = reinterpret_cast<const uint32_t*>(I.enc_tables.b() + p * I.table_bytes());
     P.headers = r ? r->dev.b() : nullptr;
     P.k = k;
     P.m = m;
-    P.w = kGfBits;
+    P.w = static_cast<uint32_t>(I.code.w);
     P.row0 = p * kRowsPerPass;
     P.nrows = std::min<uint32_t>(kRowsPerPass, m - P.row0);
     P.bs = static_cast<uint32_t>(bs);
@@ -493,8 +541,7 @@ using namespace ecamd;
 extern "C" {
 
 int liberasurecode_backend_available(const ec_backend_id_t backend_id) {
-  if (backend_id != EC_BACKEND_LIBERASURECODE_RS_VAND && backend_id != EC_BACKEND_AMD_RS_VAND)
-    return 0;
+  if (code_of(backend_id) == nullptr) return 0;
   return gpu_available();
 }
 
@@ -503,8 +550,8 @@ int liberasurecode_instance_create(const ec_backend_id_t id, struct ec_args* arg
   if (args->k < 0 || args->m < 0) return -EINVALIDPARAMS;
   if (args->k + args->m > kMaxFragments) return -EINVALIDPARAMS;
   if (static_cast<int>(id) < 0 || id >= EC_BACKENDS_MAX) return -EBACKENDNOTSUPP;
-  if (id != EC_BACKEND_LIBERASURECODE_RS_VAND && id != EC_BACKEND_AMD_RS_VAND)
-    return -EBACKENDNOTAVAIL;
+  const Code* code = code_of(id);
+  if (code == nullptr) return -EBACKENDNOTAVAIL;
   if (args->k < 1 || args->m < 1) return -EBACKENDINITERR;
   if (args->ct != CHKSUM_NONE && args->ct != CHKSUM_CRC32 && args->ct != 0)
     return -EINVALIDPARAMS;
@@ -515,28 +562,31 @@ int liberasurecode_instance_create(const ec_backend_id_t id, struct ec_args* arg
   I->m = args->m;
   I->ct = args->ct == CHKSUM_CRC32 ? CHKSUM_CRC32 : CHKSUM_NONE;
   I->backend_id = id;
+  I->code = *code;
   I->legacy_crc = write_legacy_crc();
   I->passes = (I->m + kRowsPerPass - 1) / kRowsPerPass;
   if (hipGetDevice(&I->device) != hipSuccess) return -EBACKENDNOTAVAIL;
-  I->gen = make_generator(I->k, I->m);
+  I->gen = id == EC_BACKEND_ISA_L_RS_CAUCHY ? make_isal_cauchy_matrix(I->k, I->m)
+           : id == EC_BACKEND_ISA_L_RS_VAND   ? make_isal_rs_matrix(I->k, I->m)
+                                              : make_generator(I->k, I->m);
   {
     DeviceGuard g(I->device);
     if (hipStreamCreateWithFlags(&I->stream, hipStreamNonBlocking) != hipSuccess)
       return -EBACKENDINITERR;
-    const size_t words = I->table_words();
-    std::vector<uint64_t> host(words * I->passes, 0);
+    const size_t set_bytes = I->table_bytes();
+    std::vector<uint8_t> host(set_bytes * I->passes, 0);
     for (uint32_t p = 0; p < I->passes; ++p) {
       const int r0 = p * kRowsPerPass;
       const int nr = std::min(kRowsPerPass, I->m - r0);
-      build_nibble_tables(&I->gen[static_cast<size_t>(I->k + r0) * I->k], nr, I->k,
-                          &host[p * words]);
+      build_tables(I->code.w, &I->gen[static_cast<size_t>(I->k + r0) * I->k], nr, I->k,
+                   &host[p * set_bytes]);
     }
-    hipError_t e = I->enc_tables.ensure(host.size() * 8);
+    hipError_t e = I->enc_tables.ensure(host.size());
     if (e == hipSuccess)
-      e = hipMemcpy(I->enc_tables.p, host.data(), host.size() * 8, hipMemcpyHostToDevice);
+      e = hipMemcpy(I->enc_tables.p, host.data(), host.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_errno(e);
   }
-  args->w = kGfBits;
+  args->w = I->code.w;
   std::lock_guard<std::mutex> lk(g_registry_mu);
   const int desc = ++g_next_desc;
   g_registry.emplace(desc, std::move(I));
@@ -564,7 +614,7 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
   const int k = I->k, m = I->m;
-  const uint64_t bs = blocksize_of(k, orig_data_size);
+  const uint64_t bs = blocksize_of(k, I->code.w, orig_data_size);
   const uint64_t fl = bs + kHeaderBytes;
   char** dat = static_cast<char**>(std::calloc(k, sizeof(char*)));
   char** par = static_cast<char**>(std::calloc(m, sizeof(char*)));
@@ -610,11 +660,11 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
     if ((e = hipStreamSynchronize(I->stream)) != hipSuccess) return fail(hip_errno(e));
   }
   for (int j = 0; j < k; ++j)
-    make_header(reinterpret_cast<uint8_t*>(dat[j]), j, static_cast<uint32_t>(bs),
+    make_header(reinterpret_cast<uint8_t*>(dat[j]), I->code, j, static_cast<uint32_t>(bs),
                 orig_data_size, I->ct, reinterpret_cast<uint8_t*>(dat[j]) + kHeaderBytes,
                 I->legacy_crc);
   for (int p = 0; p < m; ++p)
-    make_header(reinterpret_cast<uint8_t*>(par[p]), k + p, static_cast<uint32_t>(bs),
+    make_header(reinterpret_cast<uint8_t*>(par[p]), I->code, k + p, static_cast<uint32_t>(bs),
                 orig_data_size, I->ct, reinterpret_cast<uint8_t*>(par[p]) + kHeaderBytes,
                 I->legacy_crc);
   *encoded_data = dat;
@@ -650,11 +700,11 @@ bool payload_chksum_mismatch(const uint8_t* frag) {
 }
 
 // is_invalid_fragment (upstream erasurecode.c), used by force_metadata_checks
-bool fragment_invalid(const uint8_t* frag) {
+bool fragment_invalid(const uint8_t* frag, uint8_t wire_id) {
   const uint32_t ver = get32(frag + 63);
   if (ver > kLibecVersion) return true;
   if (get32(frag + 59) != LIBERASURECODE_FRAG_HEADER_MAGIC) return true;
-  if (frag[54] != kWireBackendId) return true;
+  if (frag[54] != wire_id) return true;
   if (frag[20] < CHKSUM_NONE || frag[20] > CHKSUM_MD5) return true;
   if (frag[53] == 1) return true;
   return payload_chksum_mismatch(frag);
@@ -715,7 +765,8 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
   if (force_metadata_checks) {
     int bad = 0;
     for (int i = 0; i < num_fragments; ++i)
-      bad += fragment_invalid(reinterpret_cast<const uint8_t*>(available_fragments[i]));
+      bad += fragment_invalid(reinterpret_cast<const uint8_t*>(available_fragments[i]),
+                              I->code.wire_id);
     if (num_fragments - bad < k) return -EINSUFFFRAGS;
   }
   // fragments_to_string preconditions: consistent orig_data_size
@@ -832,7 +883,7 @@ int liberasurecode_reconstruct_fragment(int desc, char** available_fragments, in
     if ((e = hipStreamSynchronize(I->stream)) != hipSuccess && rc == 0) rc = hip_errno(e);
     if (rc < 0) return rc;
   }
-  make_header(reinterpret_cast<uint8_t*>(out_fragment), destination_idx,
+  make_header(reinterpret_cast<uint8_t*>(out_fragment), I->code, destination_idx,
               static_cast<uint32_t>(bs), orig, I->ct,
               reinterpret_cast<uint8_t*>(out_fragment) + kHeaderBytes, I->legacy_crc);
   return 0;
@@ -876,7 +927,7 @@ int liberasurecode_verify_stripe_metadata(int desc, char** fragments, int num_fr
   for (int i = 0; i < num_fragments; ++i) {
     if (!fragments[i]) return -EINVALIDPARAMS;
     const fragment_metadata_t* md = reinterpret_cast<const fragment_metadata_t*>(fragments[i]);
-    if (md->backend_id != kWireBackendId) return -EBADHEADER;
+    if (md->backend_id != I->code.wire_id) return -EBADHEADER;
     if (md->chksum_type < CHKSUM_NONE || md->chksum_type >= CHKSUM_TYPES_MAX) return -EBADCHKSUM;
     if (md->chksum_mismatch == 1) return -EBADCHKSUM;
   }
@@ -886,7 +937,7 @@ int liberasurecode_verify_stripe_metadata(int desc, char** fragments, int num_fr
 int liberasurecode_get_aligned_data_size(int desc, uint64_t data_len) {
   auto I = lookup(desc);
   if (!I) return -EBACKENDNOTAVAIL;
-  return static_cast<int>(blocksize_of(I->k, data_len) * I->k);
+  return static_cast<int>(blocksize_of(I->k, I->code.w, data_len) * I->k);
 }
 
 int liberasurecode_get_minimum_encode_size(int desc) {
@@ -897,7 +948,7 @@ int liberasurecode_get_fragment_size(int desc, int data_len) {
   auto I = lookup(desc);
   if (!I) return -EBACKENDNOTAVAIL;
   if (data_len < 0) return -EINVALIDPARAMS;
-  return static_cast<int>(blocksize_of(I->k, static_cast<uint64_t>(data_len)));
+  return static_cast<int>(blocksize_of(I->k, I->code.w, static_cast<uint64_t>(data_len)));
 }
 
 uint32_t liberasurecode_get_version(void) { return kLibecVersion; }
@@ -906,7 +957,7 @@ uint32_t liberasurecode_get_version(void) { return kLibecVersion; }
 
 uint64_t ecamd_blocksize(int desc, uint64_t obj_len) {
   auto I = lookup(desc);
-  return I ? blocksize_of(I->k, obj_len) : 0;
+  return I ? blocksize_of(I->k, I->code.w, obj_len) : 0;
 }
 
 int ecamd_device(int desc) {
@@ -955,11 +1006,11 @@ int ecamd_reconstruct_batch(int desc, const void* d_frags, uint64_t frag_stride,
   if (I->ct == CHKSUM_CRC32) return -EBACKENDNOTSUPP;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
-  const uint64_t bs = blocksize_of(I->k, obj_len);
+  const uint64_t bs = blocksize_of(I->k, I->code.w, obj_len);
   std::vector<uint8_t> hdr(static_cast<size_t>(n_obj) * kHeaderBytes);
   for (int o = 0; o < n_obj; ++o) {
     if (h_dest[o] < 0 || h_dest[o] >= I->k + I->m) return -EINVALIDPARAMS;
-    make_header(&hdr[static_cast<size_t>(o) * kHeaderBytes], h_dest[o], static_cast<uint32_t>(bs),
+    make_header(&hdr[static_cast<size_t>(o) * kHeaderBytes], I->code, h_dest[o], static_cast<uint32_t>(bs),
                 obj_len, I->ct, nullptr, I->legacy_crc);
   }
   DecodeJob J{static_cast<const uint8_t*>(d_frags), frag_stride, stripe_stride, obj_len,

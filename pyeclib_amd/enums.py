@@ -21,5 +21,6 @@ PyECLib_FRAGHDRCHKSUM_Types = unique(
     Enum("PyECLib_FRAGHDRCHKSUM_Types", [("none", 1), ("inline_crc32", 2)], module=__name__)
 )
 
-# ec_types whose arithmetic this package runs on the GPU
-GPU_EC_TYPES = ("liberasurecode_rs_vand", "amd_rs_vand")
+# ec_types whose arithmetic this package runs on the GPU: GF(2^16) rs_vand,
+# and the GF(2^8) ISA-L Vandermonde / Cauchy codes
+GPU_EC_TYPES = ("liberasurecode_rs_vand", "amd_rs_vand", "isa_l_rs_vand", "isa_l_rs_cauchy")

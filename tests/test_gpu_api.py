@@ -40,7 +40,9 @@ def ascii_bytes(n, seed):
 
 def test_valid_ec_types_on_gpu():
     from pyeclib_amd import VALID_EC_TYPES
-    assert VALID_EC_TYPES == EC_TYPES
+    # ALL_EC_TYPES order (ec_iface.py:468-480, amd_rs_vand appended)
+    assert VALID_EC_TYPES == ["isa_l_rs_vand", "liberasurecode_rs_vand", "isa_l_rs_cauchy",
+                              "amd_rs_vand"]
 
 
 def test_use_after_close():  # test_pyeclib_api.py:386-409

@@ -125,3 +125,45 @@ def test_golden_digests(oracle, golden):
         assert hashlib.sha256(data).hexdigest() == case["data_sha256"]
         frags = oracle.encode(case["k"], case["m"], data)
         assert [hashlib.sha256(f).hexdigest() for f in frags] == case["fragments_sha256"]
+
+
+# ---------------- GF(2^8) ISA-L oracle (isal_oracle.c) ----------------
+
+@pytest.mark.parametrize("kind,name", [(4, "vand"), (7, "cauchy")])
+@pytest.mark.parametrize("k,m", [(4, 2), (10, 4), (12, 4), (8, 4), (12, 2), (11, 7)])
+def test_isal_oracle_matches_numpy(oracle, kind, name, k, m):
+    g = oracle.isal_generator(kind, k, m)
+    assert g == N.isal_generator(name, k, m)
+    assert g[:k] == [[int(i == j) for j in range(k)] for i in range(k)]
+    data = np.random.default_rng(k * 100 + m).integers(0, 256, 5003, dtype=np.uint8).tobytes()
+    frags = oracle.isal_encode(kind, k, m, data)
+    assert [f[80:] for f in frags] == N.isal_encode_payloads(name, k, m, data)
+    bs = -(-len(data) // k)  # ISA-L alignment: multiple of k bytes (w = 8)
+    assert all(len(f) == 80 + bs for f in frags)
+    for i, f in enumerate(frags):
+        assert int.from_bytes(f[0:4], "little") == i and f[54] == kind
+
+
+def test_isal_known_answers(oracle):
+    # gf_gen_rs_matrix: first parity row all ones, second row powers of 2
+    g = oracle.isal_generator(4, 6, 3)
+    assert g[6] == [1] * 6
+    assert g[7] == [1, 2, 4, 8, 16, 32]
+    assert g[8] == [1, 4, 16, 64, 29, 116]  # 4^j over 0x11D: 4^4 = 256 ^ 0x11D = 29
+    # gf_gen_cauchy1_matrix: 1 / (i ^ j); 4 * 71 = 1 in GF(2^8)/0x11D
+    c = oracle.isal_generator(7, 4, 2)
+    assert c[4][0] == 71 and oracle.isal_gf_mul(4, 71) == 1
+    assert all(oracle.isal_gf_mul(c[i][j], i ^ j) == 1 for i in (4, 5) for j in range(4))
+
+
+def test_isal_oracle_roundtrips(oracle):
+    import itertools
+    k, m = 6, 3
+    data = os.urandom(4001)
+    for kind in (4, 7):
+        frags = oracle.isal_encode(kind, k, m, data)
+        for lost in itertools.combinations(range(k + m), m):
+            avail = [f for i, f in enumerate(frags) if i not in lost]
+            assert oracle.isal_decode(kind, k, m, avail) == data
+            for i in lost:
+                assert oracle.isal_reconstruct(kind, k, m, avail, i) == frags[i]
