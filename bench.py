@@ -14,6 +14,11 @@ value = (bytes encoded + bytes decoded, all ranks) / step time, in GiB/s
 :68-99).  Objects are independent, so N GPUs each take their own batch of
 256 (weak scaling, no collective on the data path).
 
+Other BASELINE configs run through flags, each printing its own line:
+`--ec-type isa_l_rs_cauchy --k 12 --m 4 --obj-bytes 16777216 --global-batch 1024
+--second reconstruct` is configs[3] (GF(2^8) Cauchy encode + reconstruct of one
+random fragment per object, 1024 objects sharded over the GPUs).
+
 `roofline` covers the kernel that dominates a step (achieved = algorithmic
 bytes per launch / mean launch time from HIP events on the launch stream);
 `cpu_baseline` times the scalar C oracle (tests-only restatement of
@@ -33,6 +38,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "device-resident encode+decode GiB/s, k=10 m=4, 4 MiB objects, 1/2/4/8 GPU"
+FIELD_BITS = {"amd_rs_vand": 16, "liberasurecode_rs_vand": 16, "isa_l_rs_vand": 8,
+              "isa_l_rs_cauchy": 8}
 SEED = 20261015
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
@@ -49,6 +56,10 @@ def parse():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--m", type=int, default=4)
     ap.add_argument("--erasures", type=int, default=4)
+    ap.add_argument("--ec-type", default="amd_rs_vand", choices=sorted(FIELD_BITS))
+    ap.add_argument("--second", default="decode", choices=["decode", "reconstruct"],
+                    help="second half of a step: decode the batch, or rebuild one "
+                         "random fragment per object")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="objects in the CPU baseline sample (default: the full batch)")
@@ -65,6 +76,46 @@ def erasure_masks(rng, n_obj, k, m, erasures):
         lost = rng.choice(k + m, size=erasures, replace=False)
         masks.append(full & ~int(sum(1 << int(i) for i in lost)))
     return masks
+
+
+def cpu_baseline_generic(args, host_objs, masks, dests, sample):
+    """Scalar C oracle (isal_oracle.c for GF(2^8), rs_vand_oracle.c
+    otherwise), one thread: encode + decode or reconstruct per object."""
+    from oracle import oracle as O
+    k, m, n = args.k, args.m, args.obj_bytes
+    if FIELD_BITS[args.ec_type] == 8:
+        kind = O.ISAL_CAUCHY if args.ec_type == "isa_l_rs_cauchy" else O.ISAL_VAND
+        enc = lambda d: O.isal_encode(kind, k, m, d)  # noqa: E731
+        dec = lambda f: O.isal_decode(kind, k, m, f)  # noqa: E731
+        rec = lambda f, i: O.isal_reconstruct(kind, k, m, f, i)  # noqa: E731
+        src = "isal_oracle.c"
+    else:
+        enc = lambda d: O.encode(k, m, d)  # noqa: E731
+        dec = lambda f: O.decode(k, m, f)  # noqa: E731
+        rec = lambda f, i: O.reconstruct(k, m, f, i)  # noqa: E731
+        src = "rs_vand_oracle.c"
+    t_enc = t_two = 0.0
+    for o in range(sample):
+        data = host_objs[o, :n].tobytes()
+        t0 = time.perf_counter()
+        frags = enc(data)
+        t_enc += time.perf_counter() - t0
+        avail = [f for i, f in enumerate(frags) if masks[o] >> i & 1]
+        t0 = time.perf_counter()
+        if args.second == "decode":
+            assert dec(avail) == data
+        else:
+            assert rec(avail, dests[o]) == frags[dests[o]]
+        t_two += time.perf_counter() - t0
+    return {
+        "value": round(2 * sample * n / (t_enc + t_two) / 2**30, 4),
+        "unit": "GiB/s", "cores": 1, "kind": "port",
+        "sample": f"{sample} objects x {n} B: encode + {args.second} ({src}, "
+                  f"{args.ec_type}), 1 thread",
+        "encode_GiBps": round(sample * n / t_enc / 2**30, 4),
+        f"{args.second}_GiBps": round(sample * n / t_two / 2**30, 4),
+        "seconds": round(t_enc + t_two, 2),
+    }
 
 
 def cpu_baseline(args, host_objs, masks, sample):
@@ -129,7 +180,8 @@ def main():
         B = hi - lo
     else:
         B = args.batch
-    bs = batch.blocksize(k, n)
+    w = FIELD_BITS[args.ec_type]
+    bs = batch.blocksize(k, n, w)
     fs = batch.frag_stride(bs)
     obj_stride = (n + 255) // 256 * 256
 
@@ -137,16 +189,21 @@ def main():
     host = np.zeros((B, obj_stride), dtype=np.uint8)
     host[:, :n] = rng.integers(0, 256, size=(B, n), dtype=np.uint8)
     masks = erasure_masks(rng, B, k, m, args.erasures)
+    # reconstruct: one random lost fragment per object, rebuilt from the rest
+    dests = [int(d) for d in rng.integers(0, k + m, size=B)]
+    full = (1 << (k + m)) - 1
+    rmasks = [full & ~(1 << d) for d in dests]
 
-    codec = batch.BatchCodec(k, m)
+    codec = batch.BatchCodec(k, m, ec_type=args.ec_type)
     objs = torch.from_numpy(host).to(dev)
     stripes = batch.stripe_buffer(B, k, m, bs, device=dev)
     out = torch.zeros((B, obj_stride), dtype=torch.uint8, device=dev)
+    rec = torch.zeros((B, fs), dtype=torch.uint8, device=dev)
     # decode inputs: full stripes (data fragments materialised once, untimed)
     codec.encode(objs, n, parity=stripes[:, k:], data=stripes[:, :k])
     torch.cuda.synchronize()
 
-    if args.verify and rank == 0:
+    if args.verify and rank == 0 and w == 16:
         from oracle import oracle as O
         want = O.encode(k, m, host[0, :n].tobytes())
         got = stripes[0, :, :80 + bs].cpu().numpy()
@@ -163,7 +220,10 @@ def main():
         codec.encode(objs, n, parity=stripes[:, k:])
         if ev is not None:
             ev[1].record(stream)
-        codec.decode(stripes, n, masks, out)
+        if args.second == "decode":
+            codec.decode(stripes, n, masks, out)
+        else:
+            codec.reconstruct(stripes, n, rmasks, dests, rec)
         if ev is not None:
             ev[2].record(stream)
 
@@ -191,24 +251,31 @@ def main():
     # algorithmic HBM bytes per launch (DESIGN.md "Roofline"):
     #   encode: read the object (L), write m payloads + m headers
     #   decode: read k payloads, write the object
+    #   reconstruct: read k payloads, write one fragment
     enc_bytes = B * (n + m * (bs + 80))
-    dec_bytes = B * (k * bs + n)
+    two = args.second
+    two_bytes = B * (k * bs + n) if two == "decode" else B * (k * bs + bs + 80)
     kernels = {
         "encode": {"ms": round(enc_ms, 4), "bytes": enc_bytes,
                    "GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1)},
-        "decode": {"ms": round(dec_ms, 4), "bytes": dec_bytes,
-                   "GBps": round(dec_bytes / (dec_ms * 1e-3) / 1e9, 1)},
+        two: {"ms": round(dec_ms, 4), "bytes": two_bytes,
+              "GBps": round(two_bytes / (dec_ms * 1e-3) / 1e9, 1)},
     }
-    dom = "decode" if dec_ms >= enc_ms else "encode"
-    pmc = load_pmc(os.path.join(ROOT, "profiles", "pmc_summary.json")) or {}
+    dom = two if dec_ms >= enc_ms else "encode"
+    default_workload = (args.ec_type in ("amd_rs_vand", "liberasurecode_rs_vand") and k == 10
+                        and m == 4 and n == 4 * 1024 * 1024 and two == "decode")
+    pmc = (load_pmc(os.path.join(ROOT, "profiles", "pmc_summary.json")) or {}) \
+        if default_workload else {}
     traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
     achieved = kernels[dom]["GBps"]
     roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "algorithmic_bytes": kernels[dom]["bytes"]}
 
+    metric = METRIC if default_workload else (
+        f"device-resident encode+{two} GiB/s, {args.ec_type} k={k} m={m}, {n} B objects")
     result = {
-        "metric": METRIC,
+        "metric": metric,
         "value": round(value, 3),
         "unit": "GiB/s",
         "n_gpus": world,
@@ -218,20 +285,22 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if args.global_batch else "weak",
         "vs_baseline": None,
-        "dtype": "u16",
+        "dtype": "u16" if w == 16 else "u8",
         "data": f"synthetic: PCG64(seed {SEED}+rank) uniform bytes; {args.erasures} random "
                 "erasures per object for decode",
-        "config": {"workload": f"rs_vand k={k} m={m} encode + decode ({args.erasures} erasures), "
-                               f"{n} B objects, batch {B} per GPU, device-resident",
+        "config": {"workload": f"{args.ec_type} k={k} m={m} encode + "
+                               + (f"decode ({args.erasures} erasures)" if two == "decode"
+                                  else "reconstruct (1 fragment)")
+                               + f", {n} B objects, batch {B} per GPU, device-resident",
                    "k": k, "m": m, "object_bytes": n, "batch_per_gpu": B,
                    "erasures": args.erasures, "parallelism": f"objects sharded over {world} GPU"},
         "encode_GiBps": round(n_total * n / (enc_ms * 1e-3) / 2**30, 3),
-        "decode_GiBps": round(n_total * n / (dec_ms * 1e-3) / 2**30, 3),
+        f"{two}_GiBps": round(n_total * n / (dec_ms * 1e-3) / 2**30, 3),
         "kernels": kernels,
         "roofline": roofline,
     }
 
-    if args.host and rank == 0:
+    if args.host and rank == 0 and w == 16:
         pinned = torch.from_numpy(host).pin_memory()
         hpar = torch.zeros((B, m, fs), dtype=torch.uint8).pin_memory()
         codec.encode_host(pinned, n, hpar)
@@ -244,7 +313,12 @@ def main():
 
     if rank == 0 and not args.no_cpu_baseline:
         sample = args.cpu_sample or B
-        result["cpu_baseline"] = cpu_baseline(args, host, masks, min(sample, B))
+        if w == 16 and two == "decode":
+            result["cpu_baseline"] = cpu_baseline(args, host, masks, min(sample, B))
+        else:
+            masks2 = masks if two == "decode" else rmasks
+            result["cpu_baseline"] = cpu_baseline_generic(args, host, masks2, dests,
+                                                          min(sample, B))
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
