@@ -1,6 +1,7 @@
 #include "crc32.hpp"
 
 #include <cstring>
+#include <utility>
 
 namespace ecamd {
 namespace {
@@ -56,6 +57,104 @@ uint32_t crc32_legacy(uint32_t crc, const void* buf, size_t len) {
   while (len--)
     c = static_cast<int32_t>(tb.t[0][(c ^ *p++) & 0xFF]) ^ (c >> 8);  // arithmetic shift
   return static_cast<uint32_t>(c) ^ ~0u;
+}
+
+}  // namespace ecamd
+
+namespace ecamd {
+namespace {
+
+// 32x32 GF(2) matrices: column b = image of bit b.
+struct Mat {
+  uint32_t col[32];
+};
+
+uint32_t apply(const Mat& m, uint32_t r) {
+  uint32_t a = 0;
+  for (int b = 0; b < 32; ++b)
+    if (r >> b & 1) a ^= m.col[b];
+  return a;
+}
+
+Mat compose(const Mat& f, const Mat& g) {  // f(g(x))
+  Mat h;
+  for (int b = 0; b < 32; ++b) h.col[b] = apply(f, g.col[b]);
+  return h;
+}
+
+Mat identity() {
+  Mat m;
+  for (int b = 0; b < 32; ++b) m.col[b] = 1u << b;
+  return m;
+}
+
+// Z_n: append n zero bytes to the (reflected) CRC register.
+Mat zeros(uint64_t n) {
+  const Tables& tb = tables();
+  Mat one;
+  for (int b = 0; b < 32; ++b) {
+    const uint32_t r = 1u << b;
+    one.col[b] = tb.t[0][r & 0xFF] ^ (r >> 8);
+  }
+  Mat acc = identity();
+  while (n) {
+    if (n & 1) acc = compose(one, acc);
+    one = compose(one, one);
+    n >>= 1;
+  }
+  return acc;
+}
+
+bool inverse(const Mat& m, Mat& out) {
+  // rows[i] bit j = m[i][j]; augment with identity, Gauss-Jordan over GF(2)
+  uint64_t rows[32];
+  for (int i = 0; i < 32; ++i) {
+    uint32_t r = 0;
+    for (int j = 0; j < 32; ++j) r |= (m.col[j] >> i & 1u) << j;
+    rows[i] = r | (uint64_t(1) << (32 + i));
+  }
+  for (int c = 0; c < 32; ++c) {
+    int p = c;
+    while (p < 32 && !(rows[p] >> c & 1)) ++p;
+    if (p == 32) return false;
+    std::swap(rows[p], rows[c]);
+    for (int r = 0; r < 32; ++r)
+      if (r != c && (rows[r] >> c & 1)) rows[r] ^= rows[c];
+  }
+  for (int j = 0; j < 32; ++j) {
+    uint32_t col = 0;
+    for (int i = 0; i < 32; ++i) col |= static_cast<uint32_t>(rows[i] >> (32 + j) & 1) << i;
+    out.col[j] = col;
+  }
+  return true;
+}
+
+void nibble_tables(const Mat& m, uint32_t (*t)[16]) {
+  for (int q = 0; q < 8; ++q)
+    for (uint32_t v = 0; v < 16; ++v) t[q][v] = apply(m, v << (4 * q));
+}
+
+}  // namespace
+
+void build_crc_tables(uint32_t bs, uint32_t steps, CrcTables* out) {
+  const Tables& tb = tables();
+  std::memset(out, 0, sizeof(*out));
+  // raw CRC of a 16-byte chunk with byte i = v << 4h and zeros elsewhere:
+  // T0[byte] after byte i, then 15 - i zero bytes
+  Mat tail[16];
+  for (int i = 0; i < 16; ++i) tail[i] = zeros(15 - i);
+  for (int p = 0; p < 32; ++p) {
+    const int i = p / 2, h = p % 2;
+    for (uint32_t v = 0; v < 16; ++v) out->raw16[p][v] = apply(tail[i], tb.t[0][(v << (4 * h)) & 0xFF]);
+  }
+  nibble_tables(zeros(4096), out->z4096);
+  for (int l = 0; l < 8; ++l) nibble_tables(zeros(uint64_t(16) << l), out->level[l]);
+  Mat inv;
+  const uint64_t pad = uint64_t(steps) * 4096 - bs;
+  if (!inverse(zeros(pad), inv)) inv = identity();  // Z_n is always invertible (x is a unit mod P)
+  nibble_tables(inv, out->unshift);
+  for (int i = 0; i < 256; ++i) out->t0[i] = tb.t[0][i];
+  out->init_term = apply(zeros(bs), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
 }
 
 }  // namespace ecamd

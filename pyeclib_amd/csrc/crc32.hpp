@@ -18,3 +18,27 @@ uint32_t crc32(uint32_t crc, const void* buf, size_t len);
 uint32_t crc32_legacy(uint32_t crc, const void* buf, size_t len);
 
 }  // namespace ecamd
+
+namespace ecamd {
+
+// Tables for the GPU payload CRC (ec_crc.hip).  A zlib CRC-32 register is
+// GF(2)-linear in the message: with raw(M) the register after M from a zero
+// start, crc32(0, M) = raw(M) ^ Z_n(0xFFFFFFFF) ^ 0xFFFFFFFF, where Z_n
+// appends n zero bytes, and raw(A || B) = Z_|B|(raw(A)) ^ raw(B).  Every
+// linear map is stored as nibble tables [q 0..7][v 0..15] (u32) so that
+// map(r) = XOR_q T[q][nibble_q(r)] -- eight conflict-free LDS lookups.
+struct CrcTables {
+  uint32_t raw16[32][16];     // raw CRC of a 16-byte chunk, per nibble position
+  uint32_t z4096[8][16];      // Z_4096
+  uint32_t level[8][8][16];   // Z_{16 * 2^l}, l = 0..7 (lane tree)
+  uint32_t unshift[8][16];    // Z_pad^-1: drops the zero padding past the payload
+  uint32_t t0[256];           // bytewise table (header metadata CRC)
+  uint32_t init_term;         // Z_bs(0xFFFFFFFF) ^ 0xFFFFFFFF
+  uint32_t pad[3];
+};
+static_assert(sizeof(CrcTables) % 16 == 0, "CrcTables is copied to LDS in 16-B pieces");
+
+// Tables for payloads of `bs` bytes processed in `steps` rounds of 4 KiB.
+void build_crc_tables(uint32_t bs, uint32_t steps, CrcTables* out);
+
+}  // namespace ecamd

@@ -1,0 +1,148 @@
+// Inline CRC-32 of fragment payloads on the GPU (chksum_type 'inline_crc32').
+//
+// Replaces, for the batch path, what liberasurecode does on the host after
+// encoding: set_checksum (zlib crc32(0, payload, size) into chksum[0]) and
+// set_metadata_chksum (crc32 of the 59-byte metadata block at offset 67)
+// (upstream erasurecode_helpers.c; pyeclib enables it through
+// core.py:59-63 -> pyeclib_c.c:248).
+//
+// One workgroup per fragment.  Lane i owns the 16-B chunks i, i+256, ... of
+// the payload (every step is one coalesced 4 KiB read) and keeps their raw
+// CRC in Horner form acc = Z_4096(acc) ^ raw16(chunk); a tree over the 256
+// lanes (Z_{16*2^l} at level l) joins them, the zero padding past the payload
+// is removed with Z_pad^-1, and the init/final XORs are folded in at the end
+// (crc32.hpp: CrcTables).  Every linear map is 8 nibble lookups in LDS.
+#include <algorithm>
+#include <cstddef>
+
+#include "crc32.hpp"
+#include "ec_crc.hpp"
+
+namespace ecamd {
+namespace {
+
+typedef __attribute__((address_space(3))) char lds_char;
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+constexpr uint32_t kRaw16 = offsetof(CrcTables, raw16);
+constexpr uint32_t kZ4096 = offsetof(CrcTables, z4096);
+constexpr uint32_t kLevel = offsetof(CrcTables, level);
+constexpr uint32_t kUnshift = offsetof(CrcTables, unshift);
+constexpr uint32_t kT0 = offsetof(CrcTables, t0);
+constexpr uint32_t kInit = offsetof(CrcTables, init_term);
+
+__device__ __forceinline__ uint32_t lds32(uint32_t byte) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
+      reinterpret_cast<const lds_char*>(static_cast<uintptr_t>(byte)));
+}
+
+__device__ __forceinline__ uint32_t byte_of(uint32_t x, int b) { return (x >> (8 * b)) & 0xFFu; }
+
+// XOR over the 8 nibbles of r of the map's table [q][v] at LDS byte `tab`.
+__device__ __forceinline__ uint32_t zmap(uint32_t r, uint32_t tab) {
+  const uint32_t lo = (r << 2) & 0x3C3C3C3Cu, hi = (r >> 2) & 0x3C3C3C3Cu;
+  uint32_t a = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+    a ^= lds32(tab + 128 * b + byte_of(lo, b)) ^ lds32(tab + 128 * b + 64 + byte_of(hi, b));
+  return a;
+}
+
+// Raw CRC of one 16-byte chunk (32 nibble lookups).
+__device__ __forceinline__ uint32_t raw16(const uint4& x) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  uint32_t a = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t lo = (w[d] << 2) & 0x3C3C3C3Cu, hi = (w[d] >> 2) & 0x3C3C3C3Cu;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t p = 8 * d + 2 * b;  // nibble position of the byte's low nibble
+      a ^= lds32(kRaw16 + 64 * p + byte_of(lo, b)) ^ lds32(kRaw16 + 64 * (p + 1) + byte_of(hi, b));
+    }
+  }
+  return a;
+}
+
+__global__ void __launch_bounds__(256) crc_kernel(CrcParams p) {
+  {
+    auto* dst = reinterpret_cast<__attribute__((address_space(3))) v4u*>(static_cast<uintptr_t>(0));
+    const v4u* src = reinterpret_cast<const v4u*>(p.tables);
+    for (uint32_t i = threadIdx.x; i < sizeof(CrcTables) / 16; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  __attribute__((address_space(3))) uint32_t* partial =
+      reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+          static_cast<uintptr_t>(sizeof(CrcTables)));
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t total = p.n_obj * p.count;
+  for (uint32_t f = blockIdx.x; f < total; f += gridDim.x) {
+    const uint32_t o = f / p.count, i = p.first + (f - o * p.count);
+    uint8_t* frag = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + i * p.frag_stride;
+    const uint8_t* pay = frag + 80;
+    uint32_t acc = 0;
+    for (uint32_t s = 0; s < p.steps; ++s) {
+      const uint32_t off = (s * 256 + threadIdx.x) * 16;
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (off + 16 <= p.bs) {
+        const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(pay + off));
+        x = make_uint4(v.x, v.y, v.z, v.w);
+      } else if (off < p.bs) {  // payload tail: bytes past bs count as zero padding
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint32_t b = 0; off + b < p.bs; ++b)
+          w[b >> 2] |= static_cast<uint32_t>(pay[off + b]) << (8 * (b & 3));
+        x = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      acc = zmap(acc, kZ4096) ^ raw16(x);
+    }
+    // lane tree inside the wave: level l joins lanes i and i + 2^l
+#pragma unroll
+    for (int l = 0; l < 6; ++l) {
+      const uint32_t other = __shfl_down(acc, 1u << l, 64);
+      acc = zmap(acc, kLevel + 512 * l) ^ other;
+    }
+    if (lane == 0) partial[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t a = zmap(partial[0], kLevel + 512 * 6) ^ partial[1];
+      const uint32_t b = zmap(partial[2], kLevel + 512 * 6) ^ partial[3];
+      const uint32_t raw = zmap(zmap(a, kLevel + 512 * 7) ^ b, kUnshift);
+      const uint32_t crc = raw ^ lds32(kInit);
+      // header bytes 0..63: patch chksum[0] (offset 21), then the metadata
+      // checksum over bytes 0..58 (offset 67)
+      uint32_t h[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = reinterpret_cast<const uint4*>(frag)[q];
+        h[4 * q] = v.x;
+        h[4 * q + 1] = v.y;
+        h[4 * q + 2] = v.z;
+        h[4 * q + 3] = v.w;
+      }
+      // chksum occupies bytes 21..24: byte 21..23 in h[5] (bits 8..31), 24 in h[6]
+      h[5] = (h[5] & 0x000000FFu) | (crc << 8);
+      h[6] = (h[6] & 0xFFFFFF00u) | (crc >> 24);
+      uint32_t m = 0xFFFFFFFFu;
+      for (int b = 0; b < 59; ++b) m = lds32(kT0 + 4 * ((m ^ byte_of(h[b >> 2], b & 3)) & 0xFF)) ^ (m >> 8);
+      m ^= 0xFFFFFFFFu;
+      for (int b = 21; b < 25; ++b) frag[b] = static_cast<uint8_t>(crc >> (8 * (b - 21)));
+      for (int b = 67; b < 71; ++b) frag[b] = static_cast<uint8_t>(m >> (8 * (b - 67)));
+    }
+    __syncthreads();  // partial[] is reused by the next fragment
+  }
+}
+
+}  // namespace
+
+hipError_t launch_crc(const CrcParams& p, hipStream_t stream) {
+  const uint32_t total = p.n_obj * p.count;
+  if (total == 0) return hipSuccess;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint32_t grid = std::min<uint32_t>(total, static_cast<uint32_t>(cus) * 4);
+  hipLaunchKernelGGL(crc_kernel, dim3(grid), dim3(256), sizeof(CrcTables) + 16, stream, p);
+  return hipGetLastError();
+}
+
+}  // namespace ecamd

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "crc32.hpp"
+#include "ec_crc.hpp"
 #include "ec_kernels.hpp"
 #include "erasurecode_amd.h"
 #include "gf16.hpp"
@@ -100,7 +101,8 @@ void make_header(uint8_t* h, const Code& code, uint32_t idx, uint32_t bs, uint64
   put32(h + 8, 0);
   put64(h + 12, orig);
   h[20] = static_cast<uint8_t>(ct);
-  if (ct == CHKSUM_CRC32) put32(h + 21, hdr_crc(payload, bs, legacy));
+  // no payload: the GPU CRC kernel patches chksum[0] and the metadata checksum
+  if (ct == CHKSUM_CRC32 && payload) put32(h + 21, hdr_crc(payload, bs, legacy));
   h[53] = 0;
   h[54] = code.wire_id;
   put32(h + 55, code.version);
@@ -179,6 +181,7 @@ struct Instance {
   int ring_pos = 0;
   hipStream_t hstream[2] = {nullptr, nullptr};  // host-resident pipeline
   DevBuf hbuf[2];
+  std::map<uint64_t, DevBuf> crc_tables;  // payload size -> CrcTables (device)
 
   // bytes of one table set (k inputs x up to 4 rows)
   size_t table_bytes() const { return static_cast<size_t>(k) * table_bytes_per_input(code.w); }
@@ -203,6 +206,7 @@ struct Instance {
     pool.release();
     scratch.release();
     for (auto& b : hbuf) b.release();
+    for (auto& kv : crc_tables) kv.second.release();
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -471,6 +475,44 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
   return 0;
 }
 
+// Inline CRC-32 of `count` fragments per object (caller holds I.mu): payload
+// checksum and metadata checksum patched into headers already written.
+int run_crc(Instance& I, uint8_t* base, uint64_t frag_stride, uint64_t stripe_stride,
+            uint32_t count, int n_obj, uint64_t bs, hipStream_t stream) {
+  if (bs == 0 || n_obj == 0 || count == 0) return 0;
+  const uint32_t steps = static_cast<uint32_t>((bs + 4095) / 4096);
+  auto it = I.crc_tables.find(bs);
+  if (it == I.crc_tables.end()) {
+    if (I.crc_tables.size() >= 16) {  // bounded cache: wait for users, then drop it
+      (void)hipDeviceSynchronize();
+      for (auto& kv : I.crc_tables) kv.second.release();
+      I.crc_tables.clear();
+    }
+    CrcTables host;
+    build_crc_tables(static_cast<uint32_t>(bs), steps, &host);
+    DevBuf buf;
+    hipError_t e = buf.ensure(sizeof(CrcTables));
+    if (e == hipSuccess) e = hipMemcpy(buf.p, &host, sizeof(CrcTables), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      buf.release();
+      return hip_errno(e);
+    }
+    it = I.crc_tables.emplace(bs, buf).first;
+  }
+  CrcParams P{};
+  P.frags = base;
+  P.frag_stride = frag_stride;
+  P.stripe_stride = stripe_stride;
+  P.first = 0;
+  P.count = count;
+  P.n_obj = static_cast<uint32_t>(n_obj);
+  P.bs = static_cast<uint32_t>(bs);
+  P.steps = steps;
+  P.tables = it->second.p;
+  const hipError_t e = launch_crc(P, stream);
+  return e == hipSuccess ? 0 : hip_errno(e);
+}
+
 int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t obj_len, int n_obj,
                uint8_t* parity, uint8_t* data, uint64_t frag_stride, uint64_t stripe_stride,
                bool headers, hipStream_t stream) {
@@ -487,7 +529,8 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
   RingSlot* r = nullptr;
   hipError_t e;
   if (headers) {
-    if (I.ct == CHKSUM_CRC32) return -EBACKENDNOTSUPP;  // payload CRC needs the batch CRC kernel
+    // the GPU CRC writes zlib crc32 only; the legacy variant stays host-side
+    if (I.ct == CHKSUM_CRC32 && I.legacy_crc) return -EBACKENDNOTSUPP;
     r = I.ring_acquire(hdr_bytes, &e);
     if (!r) return hip_errno(e);
     for (int i = 0; i < k + m; ++i)
@@ -523,6 +566,11 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
     }
   }
   if (r && (e = I.ring_release(r, stream)) != hipSuccess) return hip_errno(e);
+  if (headers && I.ct == CHKSUM_CRC32) {
+    int rc = run_crc(I, parity, frag_stride, stripe_stride, m, n_obj, bs, stream);
+    if (rc == 0 && data) rc = run_crc(I, data, frag_stride, stripe_stride, k, n_obj, bs, stream);
+    if (rc < 0) return rc;
+  }
   return 0;
 }
 
@@ -1003,7 +1051,7 @@ int ecamd_reconstruct_batch(int desc, const void* d_frags, uint64_t frag_stride,
   auto I = lookup(desc);
   if (!I) return -EBACKENDNOTAVAIL;
   if (n_obj == 0) return 0;
-  if (I->ct == CHKSUM_CRC32) return -EBACKENDNOTSUPP;
+  if (I->ct == CHKSUM_CRC32 && I->legacy_crc) return -EBACKENDNOTSUPP;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
   const uint64_t bs = blocksize_of(I->k, I->code.w, obj_len);
@@ -1015,7 +1063,11 @@ int ecamd_reconstruct_batch(int desc, const void* d_frags, uint64_t frag_stride,
   }
   DecodeJob J{static_cast<const uint8_t*>(d_frags), frag_stride, stripe_stride, obj_len,
               static_cast<uint8_t*>(d_out), out_stride, n_obj, h_avail, h_dest, hdr.data()};
-  return run_decode(*I, J, static_cast<hipStream_t>(stream));
+  int rc = run_decode(*I, J, static_cast<hipStream_t>(stream));
+  if (rc == 0 && I->ct == CHKSUM_CRC32)
+    rc = run_crc(*I, static_cast<uint8_t*>(d_out), 0, out_stride, 1, n_obj, bs,
+                 static_cast<hipStream_t>(stream));
+  return rc;
 }
 
 int ecamd_encode_host_batch(int desc, const void* h_objs, uint64_t obj_stride, uint64_t obj_len,
