@@ -15,10 +15,9 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(\w+_kernel)(ILi(\d+)ELi(\d+)E)?", name)
-    if not m:
-        return name[:40]
-    return m.group(1) + (f"<{m.group(3)},{m.group(4)}>" if m.group(2) else "")
+    name = name.replace("ecamd::(anonymous namespace)::", "")
+    m = re.search(r"(\w+_kernel)(<[^()]*>)?", name)
+    return (m.group(1) + (m.group(2) or "")) if m else name[:40]
 
 
 def main():
