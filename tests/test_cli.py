@@ -99,7 +99,10 @@ def test_verify_gpu_schemes():
     code, out, _ = run(["verify", "--ec-type", "amd_rs_vand", "--ec-type", "isal", "-k", "6",
                         "-m", "3", "-u", "3"])
     assert code == 0, out
-    assert "amd_rs_vand     combinations=84" in out
+    # "isal" expands to every isa_l_* type; lrc / vand_inv have no GPU backend
+    for name in ("amd_rs_vand", "isa_l_rs_cauchy", "isa_l_rs_vand"):
+        assert re.search(rf"^{name} +combinations=84$", out, re.M), out
+    assert re.search(r"^isa_l_rs_lrc +not available$", out, re.M)
     code, out, _ = run(["verify", "-r", "--ec-type", "liberasurecode_rs_vand", "-k", "4", "-m",
                         "2", "-u", "2", "-i", "10"])
     assert code == 0 and "combinations=20" in out
