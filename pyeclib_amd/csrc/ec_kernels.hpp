@@ -42,9 +42,13 @@ __host__ __device__ constexpr uint32_t table_slot_bytes(uint32_t k, uint32_t w) 
 // each launch so that tools/ab_bench.py can compare them in one process:
 // ECAMD_DEC_PLAIN_STORES=1 / ECAMD_DEC_CACHED_LOADS=1 switch decode's output
 // stores / input loads from nontemporal to the default cache policy.
+// ECAMD_DEC_REALIGN=1 stores decode's object slices as lane-shifted aligned
+// 16-B units instead of plain (misaligned) 16-B lane stores; measured slower
+// on MI355X, so off by default.
 // ECAMD_XCD=0 turns off the XCD-contiguous work split (every kernel).
 constexpr uint32_t kFlagPlainStores = 1u;
 constexpr uint32_t kFlagCachedLoads = 2u;
+constexpr uint32_t kFlagNoRealign = 4u;
 
 struct EncodeParams {
   const uint8_t* objs;      // object o at objs + o * obj_stride

@@ -528,6 +528,99 @@ __device__ __forceinline__ void st_out(uint8_t* dst, const uint4& v, uint32_t fl
     st_stream(dst, v);
 }
 
+// Realigned object stores.  Decode writes data slice j of an object at
+// j*bs + t, and bs is rarely a multiple of 16 (419,432 = 8 mod 16 at 4 MiB,
+// k = 10), so a plain 16-B store per lane straddles two 16-B units and the
+// memory pipeline splits every one of them.  The 64 lanes of an interior
+// item hold one contiguous 1 KiB run, and the misalignment S = dst mod 16 is
+// the same for all of them.  Each lane takes the last S bytes of lane - 1
+// (ds_bpermute) and stores the aligned 16-B unit that begins S bytes before
+// its own address; lane 0 writes the head (its first 16 - S bytes) and
+// lane 63 the tail (its last S bytes) with naturally aligned 8/4/2/1-B
+// stores.  Neighbouring waves' head and tail share one 16-B unit, disjoint
+// bytes.  Requires all 64 lanes active with consecutive 16-B addresses.
+
+// Bytes [FROM, FROM + N) of v stored at p, where p mod 16 == AMOD: the largest
+// naturally aligned piece each time.
+template <int FROM, int N, int AMOD>
+__device__ __forceinline__ void put_bytes(uint8_t* p, const uint4& v) {
+  if constexpr (N > 0) {
+    constexpr int sz = (AMOD % 8 == 0 && N >= 8)   ? 8
+                       : (AMOD % 4 == 0 && N >= 4) ? 4
+                       : (AMOD % 2 == 0 && N >= 2) ? 2
+                                                   : 1;
+    const uint64_t lo = v.x | (static_cast<uint64_t>(v.y) << 32);
+    const uint64_t hi = v.z | (static_cast<uint64_t>(v.w) << 32);
+    uint64_t x;
+    if constexpr (FROM == 0)
+      x = lo;
+    else if constexpr (FROM < 8)
+      x = (lo >> (8 * FROM)) | (hi << (64 - 8 * FROM));
+    else if constexpr (FROM == 8)
+      x = hi;
+    else
+      x = hi >> (8 * (FROM - 8));
+    if constexpr (sz == 8)
+      *reinterpret_cast<uint64_t*>(p) = x;
+    else if constexpr (sz == 4)
+      *reinterpret_cast<uint32_t*>(p) = static_cast<uint32_t>(x);
+    else if constexpr (sz == 2)
+      *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(x);
+    else
+      *p = static_cast<uint8_t>(x);
+    put_bytes<FROM + sz, N - sz, (AMOD + sz) % 16>(p + sz, v);
+  }
+}
+
+template <int S>
+__device__ __forceinline__ void st_shifted(uint8_t* dst, const uint4& v, const uint4& prev,
+                                           uint32_t lane, uint32_t flags) {
+  // unit byte b = concat(prev, v)[16 - S + b]
+  constexpr int st = 16 - S, d = st >> 2, r = st & 3;
+  const uint32_t w[8] = {prev.x, prev.y, prev.z, prev.w, v.x, v.y, v.z, v.w};
+  uint32_t c[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if constexpr (r == 0)
+      c[i] = w[d + i];
+    else
+      c[i] = __builtin_amdgcn_alignbyte(w[d + i + 1], w[d + i], r);
+  }
+  uint8_t* unit = dst - S;
+  if (lane != 0)
+    st_out(unit, make_uint4(c[0], c[1], c[2], c[3]), flags);
+  else
+    put_bytes<0, 16 - S, S>(dst, v);
+  if (lane == 63) put_bytes<16 - S, S, 0>(unit + 16, v);
+}
+
+__device__ __forceinline__ void st_object(uint8_t* dst, const uint4& v, uint32_t flags) {
+  const uint32_t s = __builtin_amdgcn_readfirstlane(
+      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst)) & 15u);
+  if (s == 0 || (flags & kFlagNoRealign)) {
+    st_out(dst, v, flags);
+    return;
+  }
+  const uint4 prev = make_uint4(static_cast<uint32_t>(__shfl_up(static_cast<int>(v.x), 1)),
+                                static_cast<uint32_t>(__shfl_up(static_cast<int>(v.y), 1)),
+                                static_cast<uint32_t>(__shfl_up(static_cast<int>(v.z), 1)),
+                                static_cast<uint32_t>(__shfl_up(static_cast<int>(v.w), 1)));
+  const uint32_t lane = threadIdx.x & 63u;
+  switch (s) {
+#define ECAMD_SHIFT_CASE(S) \
+  case S:                   \
+    st_shifted<S>(dst, v, prev, lane, flags); \
+    break;
+    ECAMD_SHIFT_CASE(1) ECAMD_SHIFT_CASE(2) ECAMD_SHIFT_CASE(3) ECAMD_SHIFT_CASE(4)
+    ECAMD_SHIFT_CASE(5) ECAMD_SHIFT_CASE(6) ECAMD_SHIFT_CASE(7) ECAMD_SHIFT_CASE(8)
+    ECAMD_SHIFT_CASE(9) ECAMD_SHIFT_CASE(10) ECAMD_SHIFT_CASE(11) ECAMD_SHIFT_CASE(12)
+    ECAMD_SHIFT_CASE(13) ECAMD_SHIFT_CASE(14) ECAMD_SHIFT_CASE(15)
+#undef ECAMD_SHIFT_CASE
+    default:
+      break;
+  }
+}
+
 // One interior decode / reconstruct item with inputs in `cur`; prefetches the
 // block's next item (payloads into `nxt`, its table set into `pre`).
 template <class F, int K>
@@ -568,13 +661,13 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, c
     if (q >= static_cast<int>(n_out)) break;
     uint8_t* dst = p.reconstruct ? out + kHeaderBytes + t
                                  : out + static_cast<uint64_t>(d.out_idx[q]) * bs + t;
-    st_out(dst, F::row(s, q), p.flags);
+    st_object(dst, F::row(s, q), p.flags);
   }
   if (d.copy_inputs) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const uint32_t idx = d.in_idx[j];
-      if (idx < K) st_out(out + static_cast<uint64_t>(idx) * bs + t, cur[j], p.flags);
+      if (idx < K) st_object(out + static_cast<uint64_t>(idx) * bs + t, cur[j], p.flags);
     }
   }
 }
@@ -746,7 +839,8 @@ template <class F, int K>
 hipError_t launch_decode_k(DecodeParams p, hipStream_t stream) {
   split_tiles(p.bs, p.obj_len, K, p.reconstruct != 0, p.tiles, p.first_edge);
   p.flags = (env_flag("ECAMD_DEC_PLAIN_STORES", false) ? kFlagPlainStores : 0u) |
-            (env_flag("ECAMD_DEC_CACHED_LOADS", false) ? kFlagCachedLoads : 0u);
+            (env_flag("ECAMD_DEC_CACHED_LOADS", false) ? kFlagCachedLoads : 0u) |
+            (env_flag("ECAMD_DEC_REALIGN", false) ? 0u : kFlagNoRealign);
   const uint32_t interior = p.n_obj * p.first_edge;
   const uint32_t edge = p.n_obj * (p.tiles - p.first_edge);
   return launch(decode_kernel<F, K>, p, 2 * table_slot_bytes(K, F::kW), std::max(interior, edge),

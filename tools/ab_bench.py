@@ -23,7 +23,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KEYS = ("ECAMD_XCD", "ECAMD_DEC_PLAIN_STORES", "ECAMD_DEC_CACHED_LOADS")
+KEYS = ("ECAMD_XCD", "ECAMD_DEC_PLAIN_STORES", "ECAMD_DEC_CACHED_LOADS", "ECAMD_DEC_REALIGN")
 
 
 def parse_variant(text):
