@@ -3,16 +3,29 @@
 
 Metric (BASELINE.json): "device-resident encode+decode GiB/s, k=10 m=4,
 4 MiB objects, 1/2/4/8 GPU".  Workload = BASELINE configs[1] + configs[2]:
-a batch of 256 objects x 4 MiB per GPU (PCG64 seed 20261015 bytes), k=10,
-m=4, and for decode 4 random fragment erasures per object (same seed).
+a batch of 256 objects x 4 MiB per GPU (PCG64 seed 20261015 + rank bytes),
+k=10, m=4, and for decode 4 random fragment erasures per object (same seed).
 
 One step = encode the batch (objects -> 4 parity fragments with headers,
 ecamd_encode_batch) + decode the batch (first 10 of the surviving fragments
 -> objects, ecamd_decode_batch).  Inputs are resident in HBM before timing.
 value = (bytes encoded + bytes decoded, all ranks) / step time, in GiB/s
 (2^30, user object bytes, like pyeclib's own bench: src/pyeclib/cli/bench.py
-:68-99).  Objects are independent, so N GPUs each take their own batch of
-256 (weak scaling, no collective on the data path).
+:68-99, which also times encode + decode of the same segment per iteration).
+Objects are independent, so N GPUs each take their own batch of 256 (weak
+scaling, no collective on the data path; `--global-batch` shards one batch
+instead, strong scaling).
+
+`--gpus N` runs N ranks, one process per GPU: launched by the driver under
+torch.distributed.run, or -- when started directly -- bench.py starts
+torch.distributed.run itself as a child process (before anything touches the
+GPU) and exits with its status.  `--dry-run` exercises the rank launch and
+the process group on CPU (gloo) without touching a GPU.
+
+After the timed steps every object of the timed batch is checked: all k+m
+fragments (headers included) against the CPU oracle's encode, and the decoded
+(or reconstructed) output against the object (or the oracle's fragment).
+Any mismatch exits non-zero; the JSON line carries "verified": true.
 
 Other BASELINE configs run through flags, each printing its own line:
 `--ec-type isa_l_rs_cauchy --k 12 --m 4 --obj-bytes 16777216 --global-batch 1024
@@ -20,15 +33,22 @@ Other BASELINE configs run through flags, each printing its own line:
 random fragment per object, 1024 objects sharded over the GPUs).
 
 `roofline` covers the kernel that dominates a step (achieved = algorithmic
-bytes per launch / mean launch time from HIP events on the launch stream);
-`cpu_baseline` times the scalar C oracle (tests-only restatement of
-liberasurecode_rs_vand) on rank 0, single thread, over one full step's work.
+bytes per launch / mean launch time from HIP events on the launch stream) and
+lists the encode fraction beside it; `traffic` is the PMC-measured HBM bytes
+of that launch from profiles/pmc_summary.json, quoted only when that file was
+recorded on this exact library build.  `cpu_baseline` times the scalar C
+oracle (tests-only restatement of liberasurecode_rs_vand) on rank 0, over
+the same objects, in N worker processes (the reference's own scaling model:
+one single-threaded call per process, pyeclib_c.c:1245-1251) with the
+1-process figure beside it.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -42,9 +62,10 @@ FIELD_BITS = {"amd_rs_vand": 16, "liberasurecode_rs_vand": 16, "isa_l_rs_vand": 
               "isa_l_rs_cauchy": 8}
 SEED = 20261015
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+CPU_WORKERS_MAX = 16    # the GPU box's CPU share per GPU
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -63,10 +84,36 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="objects in the CPU baseline sample (default: the full batch)")
-    ap.add_argument("--host", action="store_true",
-                    help="also time the host-resident (pinned H2D/D2H) encode path")
-    ap.add_argument("--verify", action="store_true", help="check one object against the oracle")
-    return ap.parse_args()
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip checking the timed batch against the oracle (profiling runs)")
+    ap.add_argument("--no-host", action="store_true",
+                    help="skip the host-resident (pinned H2D/D2H) encode/decode timing")
+    ap.add_argument("--host", action="store_true", help=argparse.SUPPRESS)  # always on now
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch the ranks and the process group (gloo) without a GPU")
+    return ap.parse_args(argv)
+
+
+# ---------------- rank launch ----------------
+
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def relaunch_ranks(args) -> int:
+    """Start `torch.distributed.run` with one rank per GPU as a CHILD process
+    (never exec: nothing here has touched the GPU, and the ranks initialise
+    their own devices) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.call(cmd, env=env)
 
 
 def erasure_masks(rng, n_obj, k, m, erasures):
@@ -78,83 +125,180 @@ def erasure_masks(rng, n_obj, k, m, erasures):
     return masks
 
 
-def cpu_baseline_generic(args, host_objs, masks, dests, sample):
-    """Scalar C oracle (isal_oracle.c for GF(2^8), rs_vand_oracle.c
-    otherwise), one thread: encode + decode or reconstruct per object."""
-    from oracle import oracle as O
-    k, m, n = args.k, args.m, args.obj_bytes
-    if FIELD_BITS[args.ec_type] == 8:
-        kind = O.ISAL_CAUCHY if args.ec_type == "isa_l_rs_cauchy" else O.ISAL_VAND
-        enc = lambda d: O.isal_encode(kind, k, m, d)  # noqa: E731
-        dec = lambda f: O.isal_decode(kind, k, m, f)  # noqa: E731
-        rec = lambda f, i: O.isal_reconstruct(kind, k, m, f, i)  # noqa: E731
-        src = "isal_oracle.c"
-    else:
-        enc = lambda d: O.encode(k, m, d)  # noqa: E731
-        dec = lambda f: O.decode(k, m, f)  # noqa: E731
-        rec = lambda f, i: O.reconstruct(k, m, f, i)  # noqa: E731
-        src = "rs_vand_oracle.c"
-    t_enc = t_two = 0.0
-    for o in range(sample):
-        data = host_objs[o, :n].tobytes()
-        t0 = time.perf_counter()
-        frags = enc(data)
-        t_enc += time.perf_counter() - t0
-        avail = [f for i, f in enumerate(frags) if masks[o] >> i & 1]
-        t0 = time.perf_counter()
-        if args.second == "decode":
-            assert dec(avail) == data
+def first_k(mask, k, n):
+    return [i for i in range(n) if mask >> i & 1][:k]
+
+
+# ---------------- CPU oracle (checker + baseline) ----------------
+
+class OracleCodec:
+    """Raw-pointer view of the scalar C oracle for one (ec_type, k, m, L):
+    each call returns the seconds spent inside the C function only."""
+
+    def __init__(self, ec_type, k, m, n):
+        from oracle import oracle as O
+        self.O, self.k, self.m, self.n = O, k, m, n
+        self.w8 = FIELD_BITS[ec_type] == 8
+        if self.w8:
+            self.kind = O.ISAL_CAUCHY if ec_type == "isa_l_rs_cauchy" else O.ISAL_VAND
+            self.L = O.lib8()
+            self.fl = O.isal_blocksize(k, n) + O.HDR
+            self.src = "isal_oracle.c"
         else:
-            assert rec(avail, dests[o]) == frags[dests[o]]
-        t_two += time.perf_counter() - t0
-    return {
-        "value": round(2 * sample * n / (t_enc + t_two) / 2**30, 4),
-        "unit": "GiB/s", "cores": 1, "kind": "port",
-        "sample": f"{sample} objects x {n} B: encode + {args.second} ({src}, "
-                  f"{args.ec_type}), 1 thread",
-        "encode_GiBps": round(sample * n / t_enc / 2**30, 4),
-        f"{args.second}_GiBps": round(sample * n / t_two / 2**30, 4),
-        "seconds": round(t_enc + t_two, 2),
-    }
+            self.L = O.lib()
+            self.fl = O.fragment_len(k, n)
+            self.src = "rs_vand_oracle.c"
+        self.frags = np.zeros((k + m, self.fl), dtype=np.uint8)
+        self.obj = np.zeros(max(n, 1), dtype=np.uint8)
+        self.dec = np.zeros(max(n, 1), dtype=np.uint8)
+        self.rec = np.zeros(self.fl, dtype=np.uint8)
 
-
-def cpu_baseline(args, host_objs, masks, sample):
-    """Scalar C oracle, one thread: encode + decode `sample` objects."""
-    import ctypes
-    from oracle import oracle as O
-    L = O.lib()
-    k, m, n = args.k, args.m, args.obj_bytes
-    fl = O.fragment_len(k, n)
-    out = np.zeros((k + m) * fl, dtype=np.uint8)
-    obj = np.zeros(n, dtype=np.uint8)
-    t_enc = t_dec = 0.0
-    for o in range(sample):
-        obj[:] = host_objs[o, :n]
+    def encode(self, data) -> float:
+        self.obj[:self.n] = data
+        O, L = self.O, self.L
         t0 = time.perf_counter()
-        rc = L.orc_encode(k, m, O.CHKSUM_NONE, O.LIBEC_VERSION, obj.ctypes.data, n, out.ctypes.data)
-        t_enc += time.perf_counter() - t0
-        assert rc == 0
-        frags = [out[i * fl:(i + 1) * fl].tobytes() for i in range(k + m) if masks[o] >> i & 1]
-        arr = (ctypes.c_char_p * len(frags))(*frags)
-        dec = np.zeros(n, dtype=np.uint8)
+        if self.w8:
+            rc = L.o8_encode(self.kind, self.k, self.m, O.CHKSUM_NONE, O.LIBEC_VERSION,
+                             self.obj.ctypes.data, self.n, self.frags.ctypes.data)
+        else:
+            rc = L.orc_encode(self.k, self.m, O.CHKSUM_NONE, O.LIBEC_VERSION,
+                              self.obj.ctypes.data, self.n, self.frags.ctypes.data)
+        dt = time.perf_counter() - t0
+        assert rc == 0, f"oracle encode rc={rc}"
+        return dt
+
+    def _avail(self, mask):
+        idx = [i for i in range(self.k + self.m) if mask >> i & 1]
+        ptrs = (ctypes.c_void_p * len(idx))(*[self.frags[i].ctypes.data for i in idx])
+        return ctypes.cast(ptrs, ctypes.POINTER(ctypes.c_char_p)), len(idx)
+
+    def decode(self, mask) -> float:
+        arr, cnt = self._avail(mask)
         olen = ctypes.c_uint64(0)
         t0 = time.perf_counter()
-        rc = L.orc_decode(k, m, arr, len(frags), fl, dec.ctypes.data, ctypes.byref(olen))
-        t_dec += time.perf_counter() - t0
-        assert rc == 0 and olen.value == n
-    total = 2 * sample * n
-    return {
-        "value": round(total / (t_enc + t_dec) / 2**30, 4),
-        "unit": "GiB/s",
-        "cores": 1,
-        "kind": "port",
-        "sample": f"{sample} objects x {n} B: encode + decode with {args.erasures} erasures "
-                  f"each (one step's work for that many objects), scalar C oracle "
-                  f"(oracle/rs_vand_oracle.c), 1 thread",
-        "encode_GiBps": round(sample * n / t_enc / 2**30, 4),
-        "decode_GiBps": round(sample * n / t_dec / 2**30, 4),
-        "seconds": round(t_enc + t_dec, 2),
-    }
+        if self.w8:
+            rc = self.L.o8_decode(self.kind, self.k, self.m, arr, cnt, self.dec.ctypes.data,
+                                  ctypes.byref(olen))
+        else:
+            rc = self.L.orc_decode(self.k, self.m, arr, cnt, self.fl, self.dec.ctypes.data,
+                                   ctypes.byref(olen))
+        dt = time.perf_counter() - t0
+        assert rc == 0 and olen.value == self.n, f"oracle decode rc={rc}"
+        return dt
+
+    def reconstruct(self, mask, dest) -> float:
+        arr, cnt = self._avail(mask)
+        O = self.O
+        t0 = time.perf_counter()
+        if self.w8:
+            rc = self.L.o8_reconstruct(self.kind, self.k, self.m, O.CHKSUM_NONE, O.LIBEC_VERSION,
+                                       arr, cnt, self.fl, dest, self.rec.ctypes.data)
+        else:
+            rc = self.L.orc_reconstruct(self.k, self.m, O.CHKSUM_NONE, O.LIBEC_VERSION, arr,
+                                        cnt, self.fl, dest, self.rec.ctypes.data)
+        dt = time.perf_counter() - t0
+        assert rc == 0, f"oracle reconstruct rc={rc}"
+        return dt
+
+
+def oracle_pass(args, host, masks, dests, gpu_frags=None, gpu_second=None, sample=None):
+    """Run the oracle over objects [0, sample): time it, and -- when GPU
+    outputs are given -- compare every fragment (header included) and every
+    decoded object / rebuilt fragment with it.  Returns (t_enc, t_two, bad)."""
+    k, m, n = args.k, args.m, args.obj_bytes
+    oc = OracleCodec(args.ec_type, k, m, n)
+    fl = oc.fl
+    t_enc = t_two = 0.0
+    bad = []
+    for o in range(sample):
+        t_enc += oc.encode(host[o, :n])
+        if gpu_frags is not None and not np.array_equal(gpu_frags[o, :, :fl], oc.frags):
+            bad.append((o, "encode"))
+        if args.second == "decode":
+            t_two += oc.decode(masks[o])
+            if not np.array_equal(oc.dec[:n], host[o, :n]):
+                bad.append((o, "oracle decode"))
+            if gpu_second is not None and not np.array_equal(gpu_second[o, :n], host[o, :n]):
+                bad.append((o, "decode"))
+        else:
+            t_two += oc.reconstruct(masks[o], dests[o])
+            if not np.array_equal(oc.rec, oc.frags[dests[o]]):
+                bad.append((o, "oracle reconstruct"))
+            if gpu_second is not None and not np.array_equal(gpu_second[o, :fl], oc.rec):
+                bad.append((o, "reconstruct"))
+    return t_enc, t_two, bad, oc.src
+
+
+def _cpu_worker(path, shape, lo, hi, args_dict, masks, dests, barrier, q):
+    """One CPU-baseline process: encode + decode/reconstruct objects [lo, hi)
+    with the scalar oracle, after every worker is ready."""
+    host = np.memmap(path, dtype=np.uint8, mode="r", shape=shape)
+    a = argparse.Namespace(**args_dict)
+    oc = OracleCodec(a.ec_type, a.k, a.m, a.obj_bytes)
+    np.asarray(host[lo:hi]).sum()  # page the slice in before the clock starts
+    barrier.wait()
+    t0 = time.perf_counter()
+    for o in range(lo, hi):
+        oc.encode(host[o, :a.obj_bytes])
+        if a.second == "decode":
+            oc.decode(masks[o])
+        else:
+            oc.reconstruct(masks[o], dests[o])
+    q.put(time.perf_counter() - t0)
+
+
+def cpu_parallel(args, host, masks, dests, sample, workers):
+    """The oracle over objects [0, sample) in `workers` spawned processes
+    (fresh interpreters that never touch the GPU; objects shared through a
+    memory-mapped temporary file).  Returns the seconds of the slowest worker."""
+    import multiprocessing as mp
+    import tempfile
+    shape = (sample, host.shape[1])
+    fd, path = tempfile.mkstemp(prefix="ecamd_cpu_", suffix=".bin")
+    os.close(fd)
+    procs = []
+    try:
+        mm = np.memmap(path, dtype=np.uint8, mode="w+", shape=shape)
+        mm[:] = host[:sample]
+        mm.flush()
+        del mm
+        ctx = mp.get_context("spawn")
+        barrier, q = ctx.Barrier(workers), ctx.Queue()
+        keys = ("ec_type", "k", "m", "obj_bytes", "second")
+        ad = {key: getattr(args, key) for key in keys}
+        for w in range(workers):
+            lo, hi = sample * w // workers, sample * (w + 1) // workers
+            p = ctx.Process(target=_cpu_worker,
+                            args=(path, shape, lo, hi, ad, masks, dests, barrier, q))
+            p.start()
+            procs.append(p)
+        times = []
+        deadline = time.time() + 600
+        while len(times) < workers:
+            try:
+                times.append(q.get(timeout=2))
+            except Exception:  # queue.Empty
+                if time.time() > deadline or any(p.exitcode not in (None, 0) for p in procs):
+                    raise RuntimeError("CPU baseline worker failed")
+        for p in procs:
+            p.join(timeout=60)
+        return max(times)
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+        os.unlink(path)
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def load_pmc(path):
@@ -165,15 +309,77 @@ def load_pmc(path):
         return None
 
 
+# ---------------- host-resident (pinned H2D / D2H) ----------------
+
+def host_resident(args, codec, host, stripes, masks, fs, bs, reps=3):
+    """Host-resident encode and decode rates of the same batch (BASELINE
+    north_star: the path starts and ends in host memory).  Inputs and outputs
+    in pinned host memory; outputs checked against the device-resident ones."""
+    import torch
+    k, m, n = args.k, args.m, args.obj_bytes
+    B = host.shape[0]
+    out = {}
+    pinned = torch.from_numpy(host).pin_memory()
+    hpar = torch.zeros((B, m, fs), dtype=torch.uint8).pin_memory()
+    codec.encode_host(pinned, n, hpar)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        codec.encode_host(pinned, n, hpar)
+    te = (time.perf_counter() - t0) / reps
+    ok = torch.equal(hpar[:, :, :80 + bs], stripes[:, k:, :80 + bs].cpu())
+    out["host_resident_encode_GiBps"] = round(B * n / te / 2**30, 3)
+    if args.second == "decode":
+        # the k fragments each object's decode reads, as Swift would hand them over
+        idx = torch.tensor([first_k(mk, k, k + m) for mk in masks], dtype=torch.long,
+                           device=stripes.device)
+        sel = stripes[torch.arange(B, device=stripes.device)[:, None], idx]
+        hfr = torch.empty((B, k, fs), dtype=torch.uint8).pin_memory()
+        hfr.copy_(sel)
+        del sel
+        hout = torch.zeros((B, host.shape[1]), dtype=torch.uint8).pin_memory()
+        codec.decode_host(hfr, n, masks, hout)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            codec.decode_host(hfr, n, masks, hout)
+        td = (time.perf_counter() - t0) / reps
+        ok = ok and torch.equal(hout[:, :n], pinned[:, :n])
+        out["host_resident_decode_GiBps"] = round(B * n / td / 2**30, 3)
+    out["host_resident_verified"] = bool(ok)
+    out["host_resident_note"] = (f"pinned host in/out, {reps} reps of the batch; "
+                                 "H2D/kernel/D2H pipelined on 3 streams")
+    return out
+
+
+# ---------------- main ----------------
+
+def dry_run(args):
+    from pyeclib_amd import shard
+    world, rank, _ = shard.init("gloo")
+    t = shard.max_over_ranks(float(rank))
+    shard.barrier()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "requested_gpus": args.gpus,
+                          "max_rank": t}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
-    from pyeclib_amd import shard
-    world, rank, local = shard.init("nccl")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch_ranks(args))
+    if args.dry_run:
+        return dry_run(args)
     import torch
-    from pyeclib_amd import batch
-
+    from pyeclib_amd import _native, batch, shard
+    world, rank, local = shard.rank_info()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    shard.init("nccl")
+    if world != args.gpus and rank == 0:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks; "
+              f"reporting n_gpus={world}", file=sys.stderr)
     k, m, n = args.k, args.m, args.obj_bytes
     if args.global_batch:
         lo, hi = shard.shard_range(args.global_batch, rank, world)
@@ -183,6 +389,7 @@ def main():
     w = FIELD_BITS[args.ec_type]
     bs = batch.blocksize(k, n, w)
     fs = batch.frag_stride(bs)
+    fl = 80 + bs
     obj_stride = (n + 255) // 256 * 256
 
     rng = np.random.Generator(np.random.PCG64(SEED + rank))
@@ -193,6 +400,8 @@ def main():
     dests = [int(d) for d in rng.integers(0, k + m, size=B)]
     full = (1 << (k + m)) - 1
     rmasks = [full & ~(1 << d) for d in dests]
+    two = args.second
+    two_masks = masks if two == "decode" else rmasks
 
     codec = batch.BatchCodec(k, m, ec_type=args.ec_type)
     objs = torch.from_numpy(host).to(dev)
@@ -203,15 +412,6 @@ def main():
     codec.encode(objs, n, parity=stripes[:, k:], data=stripes[:, :k])
     torch.cuda.synchronize()
 
-    if args.verify and rank == 0 and w == 16:
-        from oracle import oracle as O
-        want = O.encode(k, m, host[0, :n].tobytes())
-        got = stripes[0, :, :80 + bs].cpu().numpy()
-        assert all(got[i].tobytes() == want[i] for i in range(k + m)), "encode mismatch"
-        codec.decode(stripes, n, masks, out)
-        torch.cuda.synchronize()
-        assert torch.equal(out[:, :n].cpu(), torch.from_numpy(host[:, :n])), "decode mismatch"
-
     stream = torch.cuda.current_stream()
 
     def step(ev=None):
@@ -220,7 +420,7 @@ def main():
         codec.encode(objs, n, parity=stripes[:, k:])
         if ev is not None:
             ev[1].record(stream)
-        if args.second == "decode":
+        if two == "decode":
             codec.decode(stripes, n, masks, out)
         else:
             codec.reconstruct(stripes, n, rmasks, dests, rec)
@@ -248,12 +448,11 @@ def main():
     total_bytes = 2 * n_total * n
     value = total_bytes / step_s / 2**30
 
-    # algorithmic HBM bytes per launch (DESIGN.md "Roofline"):
+    # algorithmic HBM bytes per launch:
     #   encode: read the object (L), write m payloads + m headers
     #   decode: read k payloads, write the object
     #   reconstruct: read k payloads, write one fragment
     enc_bytes = B * (n + m * (bs + 80))
-    two = args.second
     two_bytes = B * (k * bs + n) if two == "decode" else B * (k * bs + bs + 80)
     kernels = {
         "encode": {"ms": round(enc_ms, 4), "bytes": enc_bytes,
@@ -263,14 +462,22 @@ def main():
     }
     dom = two if dec_ms >= enc_ms else "encode"
     default_workload = (args.ec_type in ("amd_rs_vand", "liberasurecode_rs_vand") and k == 10
-                        and m == 4 and n == 4 * 1024 * 1024 and two == "decode")
+                        and m == 4 and n == 4 * 1024 * 1024 and two == "decode"
+                        and B == 256)
     pmc = (load_pmc(os.path.join(ROOT, "profiles", "pmc_summary.json")) or {}) \
         if default_workload else {}
-    traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch")
+    lib_id = _native.build_id()
+    pmc_ok = pmc.get("library_id") == lib_id
+    traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch") if pmc_ok else None
     achieved = kernels[dom]["GBps"]
     roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "algorithmic_bytes": kernels[dom]["bytes"]}
+                "algorithmic_bytes": kernels[dom]["bytes"],
+                "frac_by_kernel": {kk: round(v["GBps"] / HBM_PEAK_GBPS, 4)
+                                   for kk, v in kernels.items()},
+                "traffic_by_kernel": ({kk: pmc.get(kk, {}).get("hbm_bytes_per_launch")
+                                       for kk in kernels} if pmc_ok else None),
+                "library_id": lib_id}
 
     metric = METRIC if default_workload else (
         f"device-resident encode+{two} GiB/s, {args.ec_type} k={k} m={m}, {n} B objects")
@@ -300,30 +507,57 @@ def main():
         "roofline": roofline,
     }
 
-    if args.host and rank == 0 and w == 16:
-        pinned = torch.from_numpy(host).pin_memory()
-        hpar = torch.zeros((B, m, fs), dtype=torch.uint8).pin_memory()
-        codec.encode_host(pinned, n, hpar)
-        t0 = time.perf_counter()
-        reps = 3
-        for _ in range(reps):
-            codec.encode_host(pinned, n, hpar)
-        th = (time.perf_counter() - t0) / reps
-        result["host_resident_encode_GiBps"] = round(B * n / th / 2**30, 3)
+    # ---- verification of the timed batch (every object), and the CPU baseline ----
+    bad = []
+    t_enc = t_two = None
+    src = ""
+    if not args.no_verify:
+        gpu_frags = stripes[:, :, :fl].cpu().numpy()
+        gpu_second = (out[:, :n] if two == "decode" else rec[:, :fl]).cpu().numpy()
+        t_enc, t_two, bad, src = oracle_pass(args, host, two_masks, dests, gpu_frags,
+                                             gpu_second, sample=B)
+        del gpu_frags, gpu_second
+    ok = torch.tensor([0 if bad else 1], dtype=torch.int32, device=dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    verified = bool(ok.item()) and not args.no_verify
+    result["verified"] = verified
+    if not args.no_verify:
+        result["verified_objects"] = n_total
+    if bad:
+        print(f"rank {rank}: {len(bad)} mismatches vs the oracle, first: {bad[:5]}",
+              file=sys.stderr, flush=True)
+
+    if rank == 0 and not args.no_host and w == 16:
+        result.update(host_resident(args, codec, host, stripes, masks, fs, bs))
 
     if rank == 0 and not args.no_cpu_baseline:
-        sample = args.cpu_sample or B
-        if w == 16 and two == "decode":
-            result["cpu_baseline"] = cpu_baseline(args, host, masks, min(sample, B))
-        else:
-            masks2 = masks if two == "decode" else rmasks
-            result["cpu_baseline"] = cpu_baseline_generic(args, host, masks2, dests,
-                                                          min(sample, B))
+        sample = min(args.cpu_sample or B, B)
+        if t_enc is None or sample != B:
+            t_enc, t_two, _, src = oracle_pass(args, host, two_masks, dests, sample=sample)
+        workers = max(1, min(CPU_WORKERS_MAX, len(os.sched_getaffinity(0)), sample))
+        t_par = cpu_parallel(args, host, two_masks, dests, sample, workers)
+        one = 2 * sample * n / (t_enc + t_two) / 2**30
+        result["cpu_baseline"] = {
+            "value": round(2 * sample * n / t_par / 2**30, 4),
+            "unit": "GiB/s", "cores": workers, "kind": "port",
+            "sample": f"{sample} objects x {n} B: encode + {two} ({src}, {args.ec_type}), "
+                      f"{workers} single-threaded worker processes (objects split evenly)",
+            "cpu_model": cpu_model(),
+            "single_core_value": round(one, 4),
+            "single_core_encode_GiBps": round(sample * n / t_enc / 2**30, 4),
+            f"single_core_{two}_GiBps": round(sample * n / t_two / 2**30, 4),
+            "single_core_seconds": round(t_enc + t_two, 2),
+            "parallel_seconds": round(t_par, 3),
+        }
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    if not args.no_verify and not verified:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -195,10 +195,32 @@ int ecamd_reconstruct_batch(int desc, const void *d_frags, uint64_t frag_stride,
 
 /* Host-resident encode: objects in (pinned) host memory, parity fragments
  * written back to host memory; H2D / kernel / D2H pipelined over chunks of
- * objects on two streams.  Synchronous.  Parity fragment p of object o at
- * h_parity + (o*m + p)*frag_stride; objects as in ecamd_encode_batch. */
+ * objects on three streams.  Synchronous.  Parity fragment p of object o at
+ * h_parity + (o*m + p)*frag_stride; objects as in ecamd_encode_batch.
+ * Replaces, for a batch, the host side of pyeclib_c_encode
+ * (src/pyeclib_c/pyeclib_c.c:512-565): bytes in, fragments out. */
 int ecamd_encode_host_batch(int desc, const void *h_objs, uint64_t obj_stride, uint64_t obj_len,
                             int n_obj, void *h_parity, uint64_t frag_stride);
+
+/* Host-resident decode (the read path: Swift fetches k fragments per object).
+ *   h_frags:  the k fragments used for object o, in ascending fragment index,
+ *             fragment i of the group at h_frags + (o*k + i)*frag_stride
+ *             (80-byte header + payload)
+ *   h_avail:  n_obj bitmasks; the k lowest set bits name the fragments in
+ *             h_frags (liberasurecode uses the first k available)
+ *   h_objs:   output, object o at h_objs + o*obj_stride (obj_len bytes)
+ * Pipelined like ecamd_encode_host_batch; synchronous.  Replaces, for a
+ * batch, pyeclib_c_decode (src/pyeclib_c/pyeclib_c.c:770-922). */
+int ecamd_decode_host_batch(int desc, const void *h_frags, uint64_t frag_stride, uint64_t obj_len,
+                            int n_obj, const uint32_t *h_avail, void *h_objs,
+                            uint64_t obj_stride);
+
+/* Host-resident reconstruct: inputs as ecamd_decode_host_batch; fragment
+ * h_dest[o] (header included) written to h_out + o*out_stride.  Replaces,
+ * for a batch, pyeclib_c_reconstruct (src/pyeclib_c/pyeclib_c.c:681-758). */
+int ecamd_reconstruct_host_batch(int desc, const void *h_frags, uint64_t frag_stride,
+                                 uint64_t obj_len, int n_obj, const uint32_t *h_avail,
+                                 const int *h_dest, void *h_out, uint64_t out_stride);
 
 /* Device ordinal used by this process (hipGetDevice at create time). */
 int ecamd_device(int desc);

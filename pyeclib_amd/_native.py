@@ -55,6 +55,14 @@ def _share_torch_hip_runtime() -> None:
 _share_torch_hip_runtime()
 lib = ctypes.CDLL(_LIB_PATH)
 
+
+def build_id() -> str:
+    """First 16 hex digits of the SHA-256 of the loaded library file (ties
+    profiles/pmc_summary.json counters to the build they were measured on)."""
+    import hashlib
+    with open(_LIB_PATH, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
 # ---- liberasurecode constants (include/erasurecode_amd.h) ----
 EBACKENDNOTSUPP = 200
 EECMETHODNOTIMPL = 201
@@ -148,6 +156,15 @@ _sig = {
     "ecamd_encode_host_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
                                                ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
                                                ctypes.c_uint64]),
+    "ecamd_decode_host_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                               ctypes.c_uint64, ctypes.c_int,
+                                               _P(ctypes.c_uint32), ctypes.c_void_p,
+                                               ctypes.c_uint64]),
+    "ecamd_reconstruct_host_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p,
+                                                    ctypes.c_uint64, ctypes.c_uint64,
+                                                    ctypes.c_int, _P(ctypes.c_uint32),
+                                                    _P(ctypes.c_int), ctypes.c_void_p,
+                                                    ctypes.c_uint64]),
 }
 EXPORTS = tuple(_sig)
 for _name, (_res, _args) in _sig.items():

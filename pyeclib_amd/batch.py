@@ -88,6 +88,14 @@ class BatchCodec:
         if ret < 0:
             _native.raise_error(ret, fn)
 
+    @staticmethod
+    def _check_count(fn: str, n_obj: int, *arrays: Any) -> None:
+        """n_obj per-object entries must fit every tensor they index (the C
+        entry points trust the caller's sizes)."""
+        for a in arrays:
+            if a is not None and hasattr(a, "shape") and n_obj > int(a.shape[0]):
+                _native.raise_error(-_native.EINVALIDPARAMS, fn)
+
     def encode(self, objs: Any, obj_len: int, parity: Any, data: Any = None,
                frag_stride: int | None = None, stream: Any = None) -> None:
         """objs: (n_obj, obj_stride) uint8; parity: (n_obj, m, frag_stride)
@@ -95,6 +103,7 @@ class BatchCodec:
         data: optional (n_obj, k, frag_stride) view for materialised data
         fragments."""
         n_obj = int(objs.shape[0])
+        self._check_count("ecamd_encode_batch", n_obj, parity, data)
         fs = frag_stride if frag_stride is not None else int(parity.stride(1))
         ret = _native.lib.ecamd_encode_batch(
             self.handle.desc, _ptr(objs), _stride0(objs, obj_len), obj_len, n_obj,
@@ -106,6 +115,7 @@ class BatchCodec:
                stream: Any = None) -> None:
         """frags: (n_obj, k+m, frag_stride) stripes; out: (n_obj, obj_stride)."""
         n_obj = len(avail_masks)
+        self._check_count("ecamd_decode_batch", n_obj, frags, out)
         masks = (ctypes.c_uint32 * n_obj)(*avail_masks)
         fs = int(frags.stride(1))
         ret = _native.lib.ecamd_decode_batch(
@@ -117,6 +127,9 @@ class BatchCodec:
                     dest: Sequence[int], out: Any, stream: Any = None) -> None:
         """Rebuild fragment dest[o] of each object into out[o] (header included)."""
         n_obj = len(avail_masks)
+        if len(dest) != n_obj:
+            _native.raise_error(-_native.EINVALIDPARAMS, "ecamd_reconstruct_batch")
+        self._check_count("ecamd_reconstruct_batch", n_obj, frags, out)
         masks = (ctypes.c_uint32 * n_obj)(*avail_masks)
         dst = (ctypes.c_int * n_obj)(*dest)
         fs = int(frags.stride(1))
@@ -129,7 +142,38 @@ class BatchCodec:
         """Host-resident encode: objs (n_obj, obj_stride) and parity
         (n_obj, m, frag_stride) in (pinned) host memory."""
         n_obj = int(objs.shape[0])
+        self._check_count("ecamd_encode_host_batch", n_obj, parity)
         ret = _native.lib.ecamd_encode_host_batch(
             self.handle.desc, _ptr(objs), _stride0(objs, obj_len), obj_len, n_obj,
             _ptr(parity), int(parity.stride(1)))
         self._check(ret, "ecamd_encode_host_batch")
+
+    def decode_host(self, frags: Any, obj_len: int, avail_masks: Sequence[int],
+                    out: Any) -> None:
+        """Host-resident decode.  frags: (n_obj, k, frag_stride) (pinned) host
+        tensor holding, per object, the fragments named by the k lowest set
+        bits of its mask in ascending index order; out: (n_obj, obj_stride)."""
+        n_obj = len(avail_masks)
+        self._check_count("ecamd_decode_host_batch", n_obj, frags, out)
+        if hasattr(frags, "shape") and int(frags.shape[1]) != self.k:
+            _native.raise_error(-_native.EINVALIDPARAMS, "ecamd_decode_host_batch")
+        masks = (ctypes.c_uint32 * n_obj)(*avail_masks)
+        ret = _native.lib.ecamd_decode_host_batch(
+            self.handle.desc, _ptr(frags), int(frags.stride(1)), obj_len, n_obj, masks,
+            _ptr(out), _stride0(out, obj_len))
+        self._check(ret, "ecamd_decode_host_batch")
+
+    def reconstruct_host(self, frags: Any, obj_len: int, avail_masks: Sequence[int],
+                         dest: Sequence[int], out: Any) -> None:
+        """Host-resident reconstruct: inputs as decode_host; fragment dest[o]
+        (header included) into out[o] ((n_obj, frag_stride) host tensor)."""
+        n_obj = len(avail_masks)
+        if len(dest) != n_obj or (hasattr(frags, "shape") and int(frags.shape[1]) != self.k):
+            _native.raise_error(-_native.EINVALIDPARAMS, "ecamd_reconstruct_host_batch")
+        self._check_count("ecamd_reconstruct_host_batch", n_obj, frags, out)
+        masks = (ctypes.c_uint32 * n_obj)(*avail_masks)
+        dst = (ctypes.c_int * n_obj)(*dest)
+        ret = _native.lib.ecamd_reconstruct_host_batch(
+            self.handle.desc, _ptr(frags), int(frags.stride(1)), obj_len, n_obj, masks, dst,
+            _ptr(out), _stride0(out, 0))
+        self._check(ret, "ecamd_reconstruct_host_batch")

@@ -96,6 +96,8 @@ struct DecodeParams {
   uint32_t bs;
   uint32_t n_obj;
   uint32_t reconstruct;     // 1 = write fragment payload + header
+  uint32_t compact;         // 1 = input c of object o at frags + o*stripe_stride
+                            //     + c*frag_stride (only the k inputs are present)
   uint32_t tiles, first_edge;  // set by the launcher (split_tiles)
   uint32_t xcd_split;          // set by the launcher (item_range)
   uint32_t flags;              // set by the launcher (kFlag*)

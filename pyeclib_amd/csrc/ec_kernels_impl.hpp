@@ -506,6 +506,11 @@ __device__ __forceinline__ void reconstruct_header(const DecodeParams& p, const 
         p.headers + static_cast<uint64_t>(d.header) * kHeaderBytes)[threadIdx.x];
 }
 
+// Position of input c inside the object's fragment group.
+__device__ __forceinline__ uint32_t in_pos(const DecodeParams& p, const ObjDesc& d, int c) {
+  return p.compact ? static_cast<uint32_t>(c) : d.in_idx[c];
+}
+
 template <int K>
 __device__ __forceinline__ void decode_load(const DecodeParams& p, uint32_t o, uint32_t t,
                                             uint4 (&x)[K]) {
@@ -514,10 +519,10 @@ __device__ __forceinline__ void decode_load(const DecodeParams& p, uint32_t o, u
   if (p.flags & kFlagCachedLoads) {
 #pragma unroll
     for (int j = 0; j < K; ++j)
-      x[j] = *reinterpret_cast<const uint4*>(frags + d.in_idx[j] * p.frag_stride);
+      x[j] = *reinterpret_cast<const uint4*>(frags + in_pos(p, d, j) * p.frag_stride);
   } else {
 #pragma unroll
-    for (int j = 0; j < K; ++j) x[j] = ld_stream(frags + d.in_idx[j] * p.frag_stride);
+    for (int j = 0; j < K; ++j) x[j] = ld_stream(frags + in_pos(p, d, j) * p.frag_stride);
   }
 }
 
@@ -689,7 +694,7 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
   uint4 x[K];
 #pragma unroll
   for (int j = 0; j < K; ++j)
-    x[j] = *reinterpret_cast<const uint4*>(frags + d.in_idx[j] * p.frag_stride);
+    x[j] = *reinterpret_cast<const uint4*>(frags + in_pos(p, d, j) * p.frag_stride);
   typename F::Acc s;
   F::zero(s);
   if (d.n_out != 0) {

@@ -65,6 +65,7 @@ const Code* code_of(int backend_id) {
   }
 }
 constexpr int kRing = 4;
+constexpr int kHostStreams = 3;  // host-resident pipeline depth (H2D / kernel / D2H)
 
 inline uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
@@ -164,6 +165,39 @@ struct RingSlot {
   bool pending = false;
 };
 
+// Device copy of a small per-call table (decode descriptors, encode headers)
+// that usually repeats from call to call.  A call whose key differs from the
+// previous call's uploads through the ring; the second call in a row with the
+// same key uploads once into this buffer; later calls with that key launch
+// with no host work and no host-to-device copy at all.
+struct UploadCache {
+  std::vector<uint8_t> last_key;  // key of the previous call
+  std::vector<uint8_t> dev_key;   // key whose bytes are in `dev`
+  uint64_t last_gen = 0, dev_gen = 0;
+  bool dev_valid = false;
+  uint32_t dev_passes = 1;  // decode: kernel passes the cached descriptors cover
+  uint8_t* host = nullptr;
+  size_t host_cap = 0;
+  DevBuf dev;
+  hipEvent_t ev = nullptr;  // recorded after the last launch that read `dev`
+  bool pending = false;
+  hipStream_t last_stream = nullptr;
+  bool used = false;          // last_stream is meaningful
+  bool multi_stream = false;  // read from more than one stream since filled
+  void release() {
+    if (ev) {
+      (void)hipEventSynchronize(ev);
+      (void)hipEventDestroy(ev);
+      ev = nullptr;
+    }
+    if (host) (void)hipHostFree(host);
+    host = nullptr;
+    host_cap = 0;
+    dev.release();
+    dev_valid = false;
+  }
+};
+
 struct Instance {
   int k = 0, m = 0, ct = CHKSUM_NONE, backend_id = 0, device = 0;
   Code code = kRsVand;
@@ -175,12 +209,15 @@ struct Instance {
   DevBuf enc_tables;  // passes x k x 64 u64
   DevBuf pool;        // decode / reconstruct table sets
   uint32_t pool_slots = 0, pool_used = 0;
+  uint64_t pool_gen = 1;  // bumped whenever slots are recycled
   std::unordered_map<uint64_t, uint32_t> pool_index;
   DevBuf scratch;  // single-object staging
   RingSlot ring[kRing];
   int ring_pos = 0;
-  hipStream_t hstream[2] = {nullptr, nullptr};  // host-resident pipeline
-  DevBuf hbuf[2];
+  UploadCache dec_cache, rec_cache, hdr_cache;
+  hipStream_t hstream[kHostStreams] = {};  // host-resident pipeline
+  DevBuf hbuf[kHostStreams];
+  hipEvent_t hdone[kHostStreams] = {};
   std::map<uint64_t, DevBuf> crc_tables;  // payload size -> CrcTables (device)
 
   // bytes of one table set (k inputs x up to 4 rows)
@@ -194,6 +231,11 @@ struct Instance {
         (void)hipStreamSynchronize(s);
         (void)hipStreamDestroy(s);
       }
+    for (auto& e : hdone)
+      if (e) (void)hipEventDestroy(e);
+    dec_cache.release();
+    rec_cache.release();
+    hdr_cache.release();
     for (auto& r : ring) {
       if (r.ev) {
         (void)hipEventSynchronize(r.ev);
@@ -243,6 +285,92 @@ struct Instance {
     return e;
   }
 };
+
+// Where one launch's small table came from (see UploadCache).
+struct Upload {
+  const uint8_t* dev = nullptr;
+  RingSlot* ring = nullptr;     // ring slot to release after the launch, or
+  UploadCache* cache = nullptr;  // cache whose event to record after the launch
+};
+
+// Device bytes for (key, gen).  `build` fills n bytes of host memory; it is
+// only called when the bytes are not already on the device.
+template <class Build>
+int upload(Instance& I, UploadCache& C, const std::vector<uint8_t>& key, uint64_t gen, size_t n,
+           hipStream_t s, Build build, Upload* out) {
+  *out = Upload{};
+  hipError_t e;
+  if (C.dev_valid && C.dev_gen == gen && C.dev_key == key && C.dev.cap >= n) {
+    out->dev = C.dev.b();
+    out->cache = &C;
+    return 0;
+  }
+  if (C.last_key == key && C.last_gen == gen) {
+    // second call in a row with this key: make it resident, once no launch
+    // can still be reading the old bytes
+    if (C.multi_stream) {
+      if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_errno(e);
+    } else if (C.pending) {
+      if ((e = hipEventSynchronize(C.ev)) != hipSuccess) return hip_errno(e);
+    }
+    C.pending = false;
+    C.multi_stream = false;
+    C.used = false;
+    C.dev_valid = false;
+    if (!C.ev && (e = hipEventCreateWithFlags(&C.ev, hipEventDisableTiming)) != hipSuccess)
+      return hip_errno(e);
+    if (C.host_cap < n) {
+      if (C.host) (void)hipHostFree(C.host);
+      C.host = nullptr;
+      C.host_cap = 0;
+      if ((e = hipHostMalloc(reinterpret_cast<void**>(&C.host), n, 0)) != hipSuccess)
+        return hip_errno(e);
+      C.host_cap = n;
+    }
+    if ((e = C.dev.ensure(n)) != hipSuccess) return hip_errno(e);
+    int rc = build(C.host);
+    if (rc < 0) return rc;
+    if ((e = hipMemcpyAsync(C.dev.p, C.host, n, hipMemcpyHostToDevice, s)) != hipSuccess)
+      return hip_errno(e);
+    C.dev_key = key;
+    C.dev_gen = gen;
+    C.dev_valid = true;
+    out->dev = C.dev.b();
+    out->cache = &C;
+    return 0;
+  }
+  RingSlot* r = I.ring_acquire(n, &e);
+  if (!r) return hip_errno(e);
+  int rc = build(r->host);
+  if (rc < 0) return rc;
+  if ((e = I.ring_commit(r, n, s)) != hipSuccess) return hip_errno(e);
+  C.last_key = key;
+  C.last_gen = gen;
+  out->dev = r->dev.b();
+  out->ring = r;
+  return 0;
+}
+
+// After the launch(es) that read an Upload's bytes.
+hipError_t upload_done(Instance& I, Upload& u, hipStream_t s) {
+  if (u.ring) return I.ring_release(u.ring, s);
+  if (u.cache) {
+    UploadCache& C = *u.cache;
+    if (C.used && C.last_stream != s) C.multi_stream = true;
+    C.last_stream = s;
+    C.used = true;
+    hipError_t e = hipEventRecord(C.ev, s);
+    C.pending = (e == hipSuccess);
+    return e;
+  }
+  return hipSuccess;
+}
+
+template <class T>
+void key_append(std::vector<uint8_t>& key, const T* p, size_t n) {
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(p);
+  key.insert(key.end(), b, b + n * sizeof(T));
+}
 
 std::mutex g_registry_mu;
 std::map<int, std::shared_ptr<Instance>> g_registry;
@@ -330,6 +458,32 @@ bool pattern_rows(const Instance& I, const int* avail, int dest, std::vector<uin
 }
 
 // Table slot for (avail set, dest): `passes` consecutive table sets in the pool.
+// Returns kPoolFull, touching nothing, when the pattern is not cached and every
+// slot is taken: the caller must first launch the objects that already hold
+// slots, then pool_recycle() and ask again.
+constexpr int kPoolFull = 1;
+
+void missing_rows(const Instance& I, const int* avail, int dest, std::vector<int>& out_idx) {
+  if (dest >= 0) {
+    out_idx.assign(1, dest);
+    return;
+  }
+  out_idx.clear();
+  bool present[kMaxFragments] = {false};
+  for (int i = 0; i < I.k; ++i)
+    if (avail[i] < I.k) present[avail[i]] = true;
+  for (int j = 0; j < I.k; ++j)
+    if (!present[j]) out_idx.push_back(j);
+}
+
+// Wait for every launch that may read the pool, then forget all patterns.
+void pool_recycle(Instance& I) {
+  (void)hipDeviceSynchronize();
+  I.pool_index.clear();
+  I.pool_used = 0;
+  ++I.pool_gen;
+}
+
 int pool_slot(Instance& I, uint32_t avail_mask, const int* avail, int dest, uint32_t* slot,
               std::vector<int>& out_idx) {
   const uint64_t key = avail_mask | (static_cast<uint64_t>(dest + 1) << 32);
@@ -337,36 +491,26 @@ int pool_slot(Instance& I, uint32_t avail_mask, const int* avail, int dest, uint
   auto it = I.pool_index.find(key);
   if (it != I.pool_index.end()) {
     *slot = it->second;
-    // out_idx is cheap to recompute and not cached
-    if (dest >= 0) {
-      out_idx.assign(1, dest);
-    } else {
-      out_idx.clear();
-      std::vector<bool> present(I.k, false);
-      for (int i = 0; i < I.k; ++i)
-        if (avail[i] < I.k) present[avail[i]] = true;
-      for (int j = 0; j < I.k; ++j)
-        if (!present[j]) out_idx.push_back(j);
-    }
+    missing_rows(I, avail, dest, out_idx);  // cheap to recompute, not cached
     return 0;
   }
-  if (!pattern_rows(I, avail, dest, rows, out_idx)) return -EINSUFFFRAGS;
   const size_t set_bytes = I.table_bytes();
   if (I.pool_slots == 0) {
     const size_t slot_bytes = set_bytes * I.passes;
-    I.pool_slots = static_cast<uint32_t>(std::max<size_t>(64, (size_t(32) << 20) / slot_bytes));
+    // ECAMD_POOL_SLOTS (tests): force a small pool to exercise recycling
+    const char* env = std::getenv("ECAMD_POOL_SLOTS");
+    const long forced = env ? std::atol(env) : 0;
+    I.pool_slots = forced > 0 ? static_cast<uint32_t>(forced)
+                              : static_cast<uint32_t>(
+                                    std::max<size_t>(64, (size_t(32) << 20) / slot_bytes));
     hipError_t e = I.pool.ensure(slot_bytes * I.pool_slots);
     if (e != hipSuccess) {
       I.pool_slots = 0;
       return hip_errno(e);
     }
   }
-  if (I.pool_used == I.pool_slots) {
-    // Pool full: wait for every in-flight user of the pool, then recycle it.
-    (void)hipDeviceSynchronize();
-    I.pool_index.clear();
-    I.pool_used = 0;
-  }
+  if (I.pool_used == I.pool_slots) return kPoolFull;
+  if (!pattern_rows(I, avail, dest, rows, out_idx)) return -EINSUFFFRAGS;
   const uint32_t s = I.pool_used++;
   std::vector<uint8_t> host(set_bytes * I.passes, 0);
   const int nrows = static_cast<int>(out_idx.size());
@@ -401,9 +545,108 @@ struct DecodeJob {
   const uint32_t* masks;
   const int* dest;            // reconstruct: per-object destination, else null
   const uint8_t* headers;     // reconstruct: n_obj headers (host), else null
+  bool compact = false;       // object o's i-th input (ascending fragment index)
+                              // at frags + o*stripe_stride + i*frag_stride
 };
 
+// Descriptors of objects [o0, o1) of a job: `passes` arrays of (o1 - o0)
+// ObjDesc (pass p handles missing rows 4p..4p+3), then the reconstruct headers.
+struct DescBatch {
+  std::vector<ObjDesc> base;          // per object: inputs, header row
+  std::vector<uint32_t> slots;        // per object: pool slot
+  std::vector<std::vector<int>> outs; // per object: output rows (all passes)
+};
+
+size_t desc_bytes_of(const DecodeJob& J, int n, uint32_t passes) {
+  return sizeof(ObjDesc) * static_cast<size_t>(n) * passes +
+         (J.headers ? static_cast<size_t>(n) * kHeaderBytes : 0);
+}
+
+void fill_descs(const Instance& I, const DecodeJob& J, const DescBatch& B, int o0, int o1,
+                uint32_t passes, uint8_t* host) {
+  const int n = o1 - o0;
+  ObjDesc* out = reinterpret_cast<ObjDesc*>(host);
+  for (uint32_t p = 0; p < passes; ++p)
+    for (int o = o0; o < o1; ++o) {
+      ObjDesc d = B.base[o];
+      d.header = static_cast<uint32_t>(o - o0);
+      const int total = static_cast<int>(B.outs[o].size());
+      const int r0 = p * kRowsPerPass;
+      const int nr = std::max(0, std::min(kRowsPerPass, total - r0));
+      d.n_out = static_cast<uint8_t>(nr);
+      for (int r = 0; r < nr; ++r) d.out_idx[r] = static_cast<uint8_t>(B.outs[o][r0 + r]);
+      d.copy_inputs = (!J.dest && p == 0) ? 1 : 0;
+      d.table = B.slots[o] * I.passes + p;
+      out[static_cast<size_t>(p) * n + (o - o0)] = d;
+    }
+  if (J.headers)
+    std::memcpy(host + sizeof(ObjDesc) * static_cast<size_t>(n) * passes,
+                J.headers + static_cast<size_t>(o0) * kHeaderBytes,
+                static_cast<size_t>(n) * kHeaderBytes);
+}
+
+uint32_t passes_of(const DecodeJob& J, const DescBatch& B, int o0, int o1) {
+  if (J.dest) return 1;
+  size_t rows = 0;
+  for (int o = o0; o < o1; ++o) rows = std::max(rows, B.outs[o].size());
+  return std::max<uint32_t>(1, static_cast<uint32_t>((rows + kRowsPerPass - 1) / kRowsPerPass));
+}
+
+// Launch the kernel passes for objects [o0, o1) whose descriptors (passes x
+// n ObjDesc, then headers) are at `dev`.
+hipError_t launch_range(Instance& I, const DecodeJob& J, int o0, int o1, uint32_t passes,
+                        const uint8_t* dev, uint64_t bs, hipStream_t stream) {
+  const int n = o1 - o0;
+  for (uint32_t p = 0; p < passes; ++p) {
+    DecodeParams P{};
+    P.frags = J.frags + static_cast<uint64_t>(o0) * J.stripe_stride;
+    P.frag_stride = J.frag_stride;
+    P.stripe_stride = J.stripe_stride;
+    P.obj_len = J.obj_len;
+    P.out = J.out + static_cast<uint64_t>(o0) * J.out_stride;
+    P.out_stride = J.out_stride;
+    P.desc = reinterpret_cast<const ObjDesc*>(dev) + static_cast<size_t>(p) * n;
+    P.tables = reinterpret_cast<const uint32_t*>(I.pool.p);
+    P.headers = J.headers ? dev + sizeof(ObjDesc) * static_cast<size_t>(n) * passes : nullptr;
+    P.k = I.k;
+    P.m = I.m;
+    P.w = static_cast<uint32_t>(I.code.w);
+    P.bs = static_cast<uint32_t>(bs);
+    P.n_obj = static_cast<uint32_t>(n);
+    P.reconstruct = J.dest ? 1 : 0;
+    P.compact = J.compact ? 1 : 0;
+    hipError_t e = launch_decode(P, stream);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// Upload the descriptors of [o0, o1) through the ring and launch them.
+int flush_range(Instance& I, const DecodeJob& J, const DescBatch& B, int o0, int o1, uint64_t bs,
+                hipStream_t stream) {
+  if (o1 <= o0) return 0;
+  const uint32_t passes = passes_of(J, B, o0, o1);
+  const size_t n = desc_bytes_of(J, o1 - o0, passes);
+  hipError_t e;
+  RingSlot* r = I.ring_acquire(n, &e);
+  if (!r) return hip_errno(e);
+  fill_descs(I, J, B, o0, o1, passes, r->host);
+  if ((e = I.ring_commit(r, n, stream)) != hipSuccess) return hip_errno(e);
+  e = launch_range(I, J, o0, o1, passes, r->dev.b(), bs, stream);
+  const hipError_t e2 = I.ring_release(r, stream);
+  if (e != hipSuccess) return hip_errno(e);
+  return e2 == hipSuccess ? 0 : hip_errno(e2);
+}
+
 // Shared decode / reconstruct launcher (caller holds I.mu, device set).
+//
+// Every object needs the table set of its erasure pattern in the device pool.
+// When a batch brings more new patterns than the pool has free slots, the
+// objects that already hold slots are launched first, then the pool is
+// recycled (after a device-wide wait) and the rest of the batch continues --
+// a slot is never rewritten while a launched or still-to-launch object of
+// this call refers to it.  A batch whose masks repeat the previous call's
+// reuses its device descriptors (UploadCache) without rebuilding them.
 int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
   const int k = I.k, n = I.k + I.m;
   const uint64_t bs = blocksize_of(k, I.code.w, J.obj_len);
@@ -412,67 +655,71 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
   if (J.stripe_stride % 16 || reinterpret_cast<uintptr_t>(J.frags) % 16) return -EINVALIDPARAMS;
   if (J.dest && (J.out_stride % 16 || reinterpret_cast<uintptr_t>(J.out) % 16))
     return -EINVALIDPARAMS;
-  std::vector<ObjDesc> desc(static_cast<size_t>(J.n_obj));
-  std::vector<uint32_t> slots(J.n_obj);
-  std::vector<std::vector<int>> outs(J.n_obj);
-  uint32_t max_rows = 0;
+  for (int o = 0; o < J.n_obj; ++o) {
+    if (__builtin_popcount(J.masks[o] & ((n >= 32 ? 0u : (1u << n)) - 1u)) < k)
+      return -EINSUFFFRAGS;
+    if (J.dest && (J.dest[o] < 0 || J.dest[o] >= n)) return -EINVALIDPARAMS;
+  }
+
+  // cache key: everything the descriptor bytes depend on besides the pool
+  std::vector<uint8_t> key;
+  key_append(key, J.masks, J.n_obj);
+  if (J.dest) key_append(key, J.dest, J.n_obj);
+  if (J.headers) key_append(key, J.headers, static_cast<size_t>(J.n_obj) * kHeaderBytes);
+  UploadCache& C = J.dest ? I.rec_cache : I.dec_cache;
+  if (C.dev_valid && C.dev_gen == I.pool_gen && C.dev_key == key) {
+    Upload u{C.dev.b(), nullptr, &C};
+    // passes: recorded in the key's cache entry by the build below
+    const hipError_t e = launch_range(I, J, 0, J.n_obj, C.dev_passes, u.dev, bs, stream);
+    const hipError_t e2 = upload_done(I, u, stream);
+    if (e != hipSuccess) return hip_errno(e);
+    return e2 == hipSuccess ? 0 : hip_errno(e2);
+  }
+
+  DescBatch B;
+  B.base.resize(J.n_obj);
+  B.slots.resize(J.n_obj);
+  B.outs.resize(J.n_obj);
+  int o0 = 0;  // first object not yet launched
+  bool split = false;
   for (int o = 0; o < J.n_obj; ++o) {
     int avail[kMaxFragments];
-    if (first_k(J.masks[o], k, n, avail) < k) return -EINSUFFFRAGS;
+    first_k(J.masks[o], k, n, avail);
     uint32_t amask = 0;
     for (int i = 0; i < k; ++i) amask |= 1u << avail[i];
     const int dest = J.dest ? J.dest[o] : -1;
-    if (J.dest && (dest < 0 || dest >= n)) return -EINVALIDPARAMS;
-    int rc = pool_slot(I, amask, avail, dest, &slots[o], outs[o]);
+    int rc = pool_slot(I, amask, avail, dest, &B.slots[o], B.outs[o]);
+    if (rc == kPoolFull) {
+      if ((rc = flush_range(I, J, B, o0, o, bs, stream)) < 0) return rc;
+      o0 = o;
+      split = true;
+      pool_recycle(I);
+      rc = pool_slot(I, amask, avail, dest, &B.slots[o], B.outs[o]);
+      if (rc == kPoolFull) return -ENOMEM;  // pool of zero slots
+    }
     if (rc < 0) return rc;
-    ObjDesc& d = desc[o];
+    ObjDesc& d = B.base[o];
     std::memset(&d, 0, sizeof(d));
     for (int i = 0; i < k; ++i) d.in_idx[i] = static_cast<uint8_t>(avail[i]);
-    d.header = o;
-    max_rows = std::max<uint32_t>(max_rows, static_cast<uint32_t>(outs[o].size()));
   }
-  const uint32_t passes = J.dest ? 1 : std::max<uint32_t>(1, (max_rows + 3) / 4);
-  const size_t desc_bytes = sizeof(ObjDesc) * J.n_obj;
-  const size_t hdr_bytes = J.headers ? static_cast<size_t>(J.n_obj) * kHeaderBytes : 0;
-  for (uint32_t p = 0; p < passes; ++p) {
-    for (int o = 0; o < J.n_obj; ++o) {
-      ObjDesc& d = desc[o];
-      const int total = static_cast<int>(outs[o].size());
-      const int r0 = p * kRowsPerPass;
-      const int nr = std::max(0, std::min(kRowsPerPass, total - r0));
-      d.n_out = static_cast<uint8_t>(nr);
-      for (int r = 0; r < nr; ++r) d.out_idx[r] = static_cast<uint8_t>(outs[o][r0 + r]);
-      d.copy_inputs = (!J.dest && p == 0) ? 1 : 0;
-      d.table = slots[o] * I.passes + p;
-    }
-    hipError_t e;
-    RingSlot* r = I.ring_acquire(desc_bytes + hdr_bytes, &e);
-    if (!r) return hip_errno(e);
-    std::memcpy(r->host, desc.data(), desc_bytes);
-    if (hdr_bytes) std::memcpy(r->host + desc_bytes, J.headers, hdr_bytes);
-    if ((e = I.ring_commit(r, desc_bytes + hdr_bytes, stream)) != hipSuccess) return hip_errno(e);
-    DecodeParams P{};
-    P.frags = J.frags;
-    P.frag_stride = J.frag_stride;
-    P.stripe_stride = J.stripe_stride;
-    P.obj_len = J.obj_len;
-    P.out = J.out;
-    P.out_stride = J.out_stride;
-    P.desc = reinterpret_cast<const ObjDesc*>(r->dev.p);
-    P.tables = reinterpret_cast<const uint32_t*>(I.pool.p);
-    P.headers = hdr_bytes ? r->dev.b() + desc_bytes : nullptr;
-    P.k = k;
-    P.m = I.m;
-    P.w = static_cast<uint32_t>(I.code.w);
-    P.bs = static_cast<uint32_t>(bs);
-    P.n_obj = J.n_obj;
-    P.reconstruct = J.dest ? 1 : 0;
-    e = launch_decode(P, stream);
-    hipError_t e2 = I.ring_release(r, stream);
-    if (e != hipSuccess) return hip_errno(e);
-    if (e2 != hipSuccess) return hip_errno(e2);
+  if (split) {
+    C.last_key.clear();
+    return flush_range(I, J, B, o0, J.n_obj, bs, stream);
   }
-  return 0;
+  const uint32_t passes = passes_of(J, B, 0, J.n_obj);
+  Upload u;
+  int rc = upload(I, C, key, I.pool_gen, desc_bytes_of(J, J.n_obj, passes), stream,
+                  [&](uint8_t* host) {
+                    fill_descs(I, J, B, 0, J.n_obj, passes, host);
+                    return 0;
+                  },
+                  &u);
+  if (rc < 0) return rc;
+  if (u.cache) C.dev_passes = passes;
+  const hipError_t e = launch_range(I, J, 0, J.n_obj, passes, u.dev, bs, stream);
+  const hipError_t e2 = upload_done(I, u, stream);
+  if (e != hipSuccess) return hip_errno(e);
+  return e2 == hipSuccess ? 0 : hip_errno(e2);
 }
 
 // Inline CRC-32 of `count` fragments per object (caller holds I.mu): payload
@@ -526,17 +773,23 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
     return -EINVALIDPARAMS;
   if (bs > 0xFFFFFFF0ull) return -EINVALIDPARAMS;
   const size_t hdr_bytes = headers ? static_cast<size_t>(k + m) * kHeaderBytes : 0;
-  RingSlot* r = nullptr;
+  Upload u;
   hipError_t e;
   if (headers) {
     // the GPU CRC writes zlib crc32 only; the legacy variant stays host-side
     if (I.ct == CHKSUM_CRC32 && I.legacy_crc) return -EBACKENDNOTSUPP;
-    r = I.ring_acquire(hdr_bytes, &e);
-    if (!r) return hip_errno(e);
-    for (int i = 0; i < k + m; ++i)
-      make_header(r->host + i * kHeaderBytes, I.code, i, static_cast<uint32_t>(bs), obj_len, I.ct,
-                  nullptr, I.legacy_crc);
-    if ((e = I.ring_commit(r, hdr_bytes, stream)) != hipSuccess) return hip_errno(e);
+    // headers depend only on (obj_len) for a given instance
+    std::vector<uint8_t> key;
+    key_append(key, &obj_len, 1);
+    int rc = upload(I, I.hdr_cache, key, 0, hdr_bytes, stream,
+                    [&](uint8_t* host) {
+                      for (int i = 0; i < k + m; ++i)
+                        make_header(host + i * kHeaderBytes, I.code, i, static_cast<uint32_t>(bs),
+                                    obj_len, I.ct, nullptr, I.legacy_crc);
+                      return 0;
+                    },
+                    &u);
+    if (rc < 0) return rc;
   }
   for (uint32_t p = 0; p < I.passes; ++p) {
     EncodeParams P{};
@@ -548,7 +801,7 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
     P.frag_stride = frag_stride;
     P.stripe_stride = stripe_stride;
     P.tables = reinterpret_cast<const uint32_t*>(I.enc_tables.b() + p * I.table_bytes());
-    P.headers = r ? r->dev.b() : nullptr;
+    P.headers = u.dev;
     P.k = k;
     P.m = m;
     P.w = static_cast<uint32_t>(I.code.w);
@@ -561,17 +814,73 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
       break;
     }
     if ((e = launch_encode(P, stream)) != hipSuccess) {
-      if (r) (void)I.ring_release(r, stream);
+      (void)upload_done(I, u, stream);
       return hip_errno(e);
     }
   }
-  if (r && (e = I.ring_release(r, stream)) != hipSuccess) return hip_errno(e);
+  if ((e = upload_done(I, u, stream)) != hipSuccess) return hip_errno(e);
   if (headers && I.ct == CHKSUM_CRC32) {
     int rc = run_crc(I, parity, frag_stride, stripe_stride, m, n_obj, bs, stream);
     if (rc == 0 && data) rc = run_crc(I, data, frag_stride, stripe_stride, k, n_obj, bs, stream);
     if (rc < 0) return rc;
   }
   return 0;
+}
+
+// Host-resident pipelines.  The caller's objects / fragments are in (pinned)
+// host memory; chunks of objects go H2D -> kernels -> D2H, chunk c on stream
+// c % kHostStreams, so one chunk's H2D, another's kernels and a third's D2H
+// are in flight together (PCIe Gen5 x16 is full duplex: the bound is
+// max(H2D bytes, D2H bytes) / link rate).  `in` / `out` describe the host
+// arrays: object o's input at in + o*in_stride (in_last bytes for the final
+// object of a chunk), output at out + o*out_stride (out_last likewise).
+// Device staging per stream: in buffer at +kInSkew, out buffer at +kOutSkew
+// past 256-B boundaries so fragment payloads (80 B after a fragment's start)
+// and objects sit on 128-B lines when the strides are multiples of 128.
+struct HostSide {
+  const uint8_t* in;
+  uint64_t in_stride, in_last, in_skew;
+  uint8_t* out;
+  uint64_t out_stride, out_last, out_skew;
+};
+
+template <class Run>
+int host_pipeline(Instance& I, int n_obj, const HostSide& H, Run run) {
+  // ~32 MiB of input per chunk, at least kHostStreams * 2 chunks when the
+  // batch allows, so the three stages overlap for most of the batch
+  int chunk = static_cast<int>(std::max<uint64_t>(1, (uint64_t(32) << 20) / H.in_stride));
+  chunk = std::min(chunk, std::max(1, (n_obj + 2 * kHostStreams - 1) / (2 * kHostStreams)));
+  const uint64_t in_cap = (static_cast<uint64_t>(chunk) * H.in_stride + H.in_skew + 255) & ~255ull;
+  const uint64_t out_cap = static_cast<uint64_t>(chunk) * H.out_stride + H.out_skew;
+  hipError_t e = hipSuccess;
+  for (int s = 0; s < kHostStreams; ++s) {
+    if (!I.hstream[s] &&
+        (e = hipStreamCreateWithFlags(&I.hstream[s], hipStreamNonBlocking)) != hipSuccess)
+      return hip_errno(e);
+    if ((e = I.hbuf[s].ensure(in_cap + out_cap)) != hipSuccess) return hip_errno(e);
+  }
+  int rc = 0;
+  for (int o0 = 0, c = 0; o0 < n_obj && rc == 0; o0 += chunk, ++c) {
+    const int n = std::min(chunk, n_obj - o0);
+    const int si = c % kHostStreams;
+    hipStream_t s = I.hstream[si];
+    uint8_t* d_in = I.hbuf[si].b() + H.in_skew;
+    uint8_t* d_out = I.hbuf[si].b() + in_cap + H.out_skew;
+    const uint64_t nin = static_cast<uint64_t>(n - 1) * H.in_stride + H.in_last;
+    if ((e = hipMemcpyAsync(d_in, H.in + static_cast<uint64_t>(o0) * H.in_stride, nin,
+                            hipMemcpyHostToDevice, s)) != hipSuccess) {
+      rc = hip_errno(e);
+      break;
+    }
+    if ((rc = run(d_in, d_out, o0, n, s)) < 0) break;
+    const uint64_t nout = static_cast<uint64_t>(n - 1) * H.out_stride + H.out_last;
+    if ((e = hipMemcpyAsync(H.out + static_cast<uint64_t>(o0) * H.out_stride, d_out, nout,
+                            hipMemcpyDeviceToHost, s)) != hipSuccess)
+      rc = hip_errno(e);
+  }
+  for (auto s : I.hstream)
+    if (s && (e = hipStreamSynchronize(s)) != hipSuccess && rc == 0) rc = hip_errno(e);
+  return rc;
 }
 
 char* alloc_fragment(uint64_t size) {
@@ -817,10 +1126,15 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
                               I->code.wire_id);
     if (num_fragments - bad < k) return -EINSUFFFRAGS;
   }
-  // fragments_to_string preconditions: consistent orig_data_size
+  // fragments_to_string preconditions: consistent orig_data_size, and every
+  // payload size field inside the fragment buffer (a corrupt or crafted size
+  // must not make the copies below read past it)
   const uint64_t orig = get64(available_fragments[0] + 12);
-  for (int i = 1; i < num_fragments; ++i)
+  for (int i = 0; i < num_fragments; ++i) {
     if (get64(available_fragments[i] + 12) != orig) return -EBADHEADER;
+    if (static_cast<uint64_t>(get32(available_fragments[i] + 4)) + kHeaderBytes > fragment_len)
+      return -EBADHEADER;
+  }
   Partition P;
   int rc = partition(*I, available_fragments, num_fragments, P);
   bool all_data = true;
@@ -893,9 +1207,11 @@ int liberasurecode_reconstruct_fragment(int desc, char** available_fragments, in
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
   const int k = I->k, m = I->m;
+  if (fragment_len < kHeaderBytes) return -EBADHEADER;
   for (int i = 0; i < num_fragments; ++i)
     if (!available_fragments[i] ||
-        header_invalid(reinterpret_cast<const uint8_t*>(available_fragments[i])))
+        header_invalid(reinterpret_cast<const uint8_t*>(available_fragments[i])) ||
+        static_cast<uint64_t>(get32(available_fragments[i] + 4)) + kHeaderBytes > fragment_len)
       return -EBADHEADER;
   Partition P;
   int rc = partition(*I, available_fragments, num_fragments, P);
@@ -1076,44 +1392,77 @@ int ecamd_encode_host_batch(int desc, const void* h_objs, uint64_t obj_stride, u
   auto I = lookup(desc);
   if (!I) return -EBACKENDNOTAVAIL;
   if (n_obj == 0) return 0;
+  if (obj_len == 0) return -EINVALIDPARAMS;
   if (obj_stride < obj_len || obj_stride % 16 || frag_stride % 16) return -EINVALIDPARAMS;
+  const uint64_t bs = blocksize_of(I->k, I->code.w, obj_len);
+  if (frag_stride < kHeaderBytes + round16(bs)) return -EINVALIDPARAMS;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
   const int m = I->m;
-  // ~64 MiB of objects per chunk, two chunks in flight (one per stream).
-  const int chunk = static_cast<int>(std::max<uint64_t>(1, (uint64_t(64) << 20) / obj_stride));
-  const uint64_t in_bytes = static_cast<uint64_t>(chunk) * obj_stride;
-  const uint64_t out_bytes = static_cast<uint64_t>(chunk) * m * frag_stride;
-  hipError_t e = hipSuccess;
-  for (int s = 0; s < 2; ++s) {
-    if (!I->hstream[s] &&
-        (e = hipStreamCreateWithFlags(&I->hstream[s], hipStreamNonBlocking)) != hipSuccess)
-      return hip_errno(e);
-    if ((e = I->hbuf[s].ensure(in_bytes + out_bytes)) != hipSuccess) return hip_errno(e);
+  const uint64_t ps = static_cast<uint64_t>(m) * frag_stride;
+  const HostSide H{static_cast<const uint8_t*>(h_objs), obj_stride, obj_len, 0,
+                   static_cast<uint8_t*>(h_parity), ps, ps, 48};
+  return host_pipeline(*I, n_obj, H, [&](uint8_t* d_in, uint8_t* d_out, int, int n, hipStream_t s) {
+    return run_encode(*I, d_in, obj_stride, obj_len, n, d_out, nullptr, frag_stride, ps, true, s);
+  });
+}
+
+int ecamd_decode_host_batch(int desc, const void* h_frags, uint64_t frag_stride, uint64_t obj_len,
+                            int n_obj, const uint32_t* h_avail, void* h_objs,
+                            uint64_t obj_stride) {
+  if (!h_frags || !h_avail || !h_objs || n_obj < 0) return -EINVALIDPARAMS;
+  auto I = lookup(desc);
+  if (!I) return -EBACKENDNOTAVAIL;
+  if (n_obj == 0) return 0;
+  if (obj_len == 0 || obj_stride < obj_len || obj_stride % 16 || frag_stride % 16)
+    return -EINVALIDPARAMS;
+  const uint64_t bs = blocksize_of(I->k, I->code.w, obj_len);
+  if (frag_stride < kHeaderBytes + round16(bs)) return -EINVALIDPARAMS;
+  std::lock_guard<std::mutex> lk(I->mu);
+  DeviceGuard g(I->device);
+  const uint64_t gs = static_cast<uint64_t>(I->k) * frag_stride;
+  const HostSide H{static_cast<const uint8_t*>(h_frags), gs, gs, 48,
+                   static_cast<uint8_t*>(h_objs), obj_stride, obj_len, 0};
+  return host_pipeline(*I, n_obj, H, [&](uint8_t* d_in, uint8_t* d_out, int o0, int n,
+                                         hipStream_t s) {
+    DecodeJob J{d_in, frag_stride, gs, obj_len, d_out, obj_stride, n, h_avail + o0,
+                nullptr, nullptr, true};
+    return run_decode(*I, J, s);
+  });
+}
+
+int ecamd_reconstruct_host_batch(int desc, const void* h_frags, uint64_t frag_stride,
+                                 uint64_t obj_len, int n_obj, const uint32_t* h_avail,
+                                 const int* h_dest, void* h_out, uint64_t out_stride) {
+  if (!h_frags || !h_avail || !h_dest || !h_out || n_obj < 0) return -EINVALIDPARAMS;
+  auto I = lookup(desc);
+  if (!I) return -EBACKENDNOTAVAIL;
+  if (n_obj == 0) return 0;
+  if (I->ct == CHKSUM_CRC32 && I->legacy_crc) return -EBACKENDNOTSUPP;
+  const uint64_t bs = blocksize_of(I->k, I->code.w, obj_len);
+  if (obj_len == 0 || frag_stride % 16 || out_stride % 16 ||
+      frag_stride < kHeaderBytes + round16(bs) || out_stride < kHeaderBytes + round16(bs))
+    return -EINVALIDPARAMS;
+  std::lock_guard<std::mutex> lk(I->mu);
+  DeviceGuard g(I->device);
+  std::vector<uint8_t> hdr(static_cast<size_t>(n_obj) * kHeaderBytes);
+  for (int o = 0; o < n_obj; ++o) {
+    if (h_dest[o] < 0 || h_dest[o] >= I->k + I->m) return -EINVALIDPARAMS;
+    make_header(&hdr[static_cast<size_t>(o) * kHeaderBytes], I->code, h_dest[o],
+                static_cast<uint32_t>(bs), obj_len, I->ct, nullptr, I->legacy_crc);
   }
-  int rc = 0;
-  for (int o0 = 0, c = 0; o0 < n_obj && rc == 0; o0 += chunk, ++c) {
-    const int n = std::min(chunk, n_obj - o0);
-    hipStream_t s = I->hstream[c & 1];
-    uint8_t* d_in = I->hbuf[c & 1].b();
-    uint8_t* d_out = d_in + in_bytes;
-    const uint8_t* src = static_cast<const uint8_t*>(h_objs) + static_cast<uint64_t>(o0) * obj_stride;
-    const uint64_t nin = static_cast<uint64_t>(n - 1) * obj_stride + obj_len;
-    if ((e = hipMemcpyAsync(d_in, src, nin, hipMemcpyHostToDevice, s)) != hipSuccess) {
-      rc = hip_errno(e);
-      break;
-    }
-    rc = run_encode(*I, d_in, obj_stride, obj_len, n, d_out, nullptr, frag_stride,
-                    static_cast<uint64_t>(m) * frag_stride, true, s);
-    if (rc < 0) break;
-    uint8_t* dst = static_cast<uint8_t*>(h_parity) + static_cast<uint64_t>(o0) * m * frag_stride;
-    if ((e = hipMemcpyAsync(dst, d_out, static_cast<uint64_t>(n) * m * frag_stride,
-                            hipMemcpyDeviceToHost, s)) != hipSuccess)
-      rc = hip_errno(e);
-  }
-  for (auto s : I->hstream)
-    if ((e = hipStreamSynchronize(s)) != hipSuccess && rc == 0) rc = hip_errno(e);
-  return rc;
+  const uint64_t gs = static_cast<uint64_t>(I->k) * frag_stride;
+  const HostSide H{static_cast<const uint8_t*>(h_frags), gs, gs, 48,
+                   static_cast<uint8_t*>(h_out), out_stride, kHeaderBytes + bs, 48};
+  return host_pipeline(*I, n_obj, H, [&](uint8_t* d_in, uint8_t* d_out, int o0, int n,
+                                         hipStream_t s) {
+    DecodeJob J{d_in, frag_stride, gs, obj_len, d_out, out_stride, n, h_avail + o0,
+                h_dest + o0, hdr.data() + static_cast<size_t>(o0) * kHeaderBytes, true};
+    int rc = run_decode(*I, J, s);
+    if (rc == 0 && I->ct == CHKSUM_CRC32)
+      rc = run_crc(*I, d_out, 0, out_stride, 1, n, bs, s);
+    return rc;
+  });
 }
 
 }  // extern "C"

@@ -18,6 +18,10 @@ for s in $STEPS; do
     (cd $R && timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
         --timeout-method thread > $O/pytest_gpu.log 2>&1)
     tail -3 $O/pytest_gpu.log ;;
+  newtests)
+    (cd $R && timeout -k 10 600 python3 -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 300 \
+        --timeout-method thread > $O/pytest_gpu_new.log 2>&1)
+    tail -3 $O/pytest_gpu_new.log ;;
   smoke)
     (cd $R && timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1)
     tail -1 $O/smoke.log ;;
@@ -27,23 +31,23 @@ for s in $STEPS; do
         ECAMD_XCD=0,ECAMD_DEC_PLAIN_STORES=1 > $O/ab.txt 2>&1)
     cat $O/ab.txt ;;
   bench)
-    (cd $R && timeout -k 10 400 python3 bench.py --host > $O/bench.json 2> $O/bench.err)
+    (cd $R && timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err)
     cat $O/bench.json ;;
   prof)
     (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run \
-      -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/prof_bench.json 2> $O/prof.err)
+      -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-verify --no-host > $O/prof_bench.json 2> $O/prof.err)
     cat $O/prof_bench.json
     find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \; ;;
   pmc)
     (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run \
-      -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_fetch.log 2>&1)
+      -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host > $O/pmc_fetch.log 2>&1)
     (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run \
-      -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/pmc_write.log 2>&1)
+      -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host > $O/pmc_write.log 2>&1)
     python3 $R/tools/pmc_summary.py $O/pmc_fetch $O/pmc_write $O/pmc_summary.json ;;
   sq)
     for f in pmc1 pmc2; do
       (cd /tmp && timeout -s KILL 150 rocprofv3 -i $R/tools/$f.txt --output-format csv -d $O/sq_$f -o run \
-        -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/sq_$f.log 2>&1)
+        -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host > $O/sq_$f.log 2>&1)
     done
     python3 $R/tools/pmc_table.py $O/sq_pmc1 $O/sq_pmc2 > $O/sq_table.txt 2>&1 || true
     cat $O/sq_table.txt ;;

@@ -41,11 +41,20 @@ def load(path, counter):
     return out
 
 
+def library_id():
+    """Build id of the profiled library (same as pyeclib_amd._native.build_id):
+    bench.py quotes these counters only while the library is unchanged."""
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "pyeclib_amd", "libpyeclib_amd.so"), "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()[:16]
+
+
 def main():
     fetch_dir, write_dir, dst = sys.argv[1:4]
     fetch = load(fetch_dir, "FETCH_SIZE")
     write = load(write_dir, "WRITE_SIZE")
-    summary = {}
+    summary = {"library_id": library_id()}
     for op in sorted(set(fetch) | set(write)):
         f_kib, w_kib = fetch.get(op, 0.0), write.get(op, 0.0)
         summary[op] = {
