@@ -183,12 +183,20 @@ struct UploadCache {
   bool pending = false;
   hipStream_t last_stream = nullptr;
   bool used = false;          // last_stream is meaningful
+  hipEvent_t fill_ev = nullptr;     // recorded after the H2D copy that filled `dev`
+  hipStream_t fill_stream = nullptr;
+  bool fill_done = false;           // that copy is known to be complete
   bool multi_stream = false;  // read from more than one stream since filled
   void release() {
     if (ev) {
       (void)hipEventSynchronize(ev);
       (void)hipEventDestroy(ev);
       ev = nullptr;
+    }
+    if (fill_ev) {
+      (void)hipEventSynchronize(fill_ev);
+      (void)hipEventDestroy(fill_ev);
+      fill_ev = nullptr;
     }
     if (host) (void)hipHostFree(host);
     host = nullptr;
@@ -293,6 +301,18 @@ struct Upload {
   UploadCache* cache = nullptr;  // cache whose event to record after the launch
 };
 
+// A launch on stream s may read the cache's device bytes only after the copy
+// that filled them, which ran on C.fill_stream: other streams wait for it on
+// the GPU (no host wait) until it is known to be complete.
+hipError_t cache_ready(UploadCache& C, hipStream_t s) {
+  if (C.fill_done) return hipSuccess;
+  if (hipEventQuery(C.fill_ev) == hipSuccess) {
+    C.fill_done = true;
+    return hipSuccess;
+  }
+  return s == C.fill_stream ? hipSuccess : hipStreamWaitEvent(s, C.fill_ev, 0);
+}
+
 // Device bytes for (key, gen).  `build` fills n bytes of host memory; it is
 // only called when the bytes are not already on the device.
 template <class Build>
@@ -301,6 +321,7 @@ int upload(Instance& I, UploadCache& C, const std::vector<uint8_t>& key, uint64_
   *out = Upload{};
   hipError_t e;
   if (C.dev_valid && C.dev_gen == gen && C.dev_key == key && C.dev.cap >= n) {
+    if ((e = cache_ready(C, s)) != hipSuccess) return hip_errno(e);
     out->dev = C.dev.b();
     out->cache = &C;
     return 0;
@@ -332,6 +353,11 @@ int upload(Instance& I, UploadCache& C, const std::vector<uint8_t>& key, uint64_
     if (rc < 0) return rc;
     if ((e = hipMemcpyAsync(C.dev.p, C.host, n, hipMemcpyHostToDevice, s)) != hipSuccess)
       return hip_errno(e);
+    if (!C.fill_ev && (e = hipEventCreateWithFlags(&C.fill_ev, hipEventDisableTiming)) != hipSuccess)
+      return hip_errno(e);
+    if ((e = hipEventRecord(C.fill_ev, s)) != hipSuccess) return hip_errno(e);
+    C.fill_stream = s;
+    C.fill_done = false;
     C.dev_key = key;
     C.dev_gen = gen;
     C.dev_valid = true;
@@ -668,6 +694,8 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
   if (J.headers) key_append(key, J.headers, static_cast<size_t>(J.n_obj) * kHeaderBytes);
   UploadCache& C = J.dest ? I.rec_cache : I.dec_cache;
   if (C.dev_valid && C.dev_gen == I.pool_gen && C.dev_key == key) {
+    hipError_t ew = cache_ready(C, stream);
+    if (ew != hipSuccess) return hip_errno(ew);
     Upload u{C.dev.b(), nullptr, &C};
     // passes: recorded in the key's cache entry by the build below
     const hipError_t e = launch_range(I, J, 0, J.n_obj, C.dev_passes, u.dev, bs, stream);
