@@ -32,23 +32,14 @@ __host__ __device__ constexpr uint32_t table_bytes_per_input(uint32_t w) {
   return w == 16 ? 512u : 128u;
 }
 
-// Decode keeps two table sets in LDS; a slot is rounded up to 256 B so that
-// its base fits the second byte of an LDS address (ec_kernels_impl.hpp, kb).
+// Decode keeps one table set per wave in LDS; a slot is rounded up to 256 B
+// so that its base fits the second byte of an LDS address (ec_kernels_impl.hpp,
+// kb), and 4 slots of the largest set (k = 31, GF(2^16)) stay below 64 KiB.
 __host__ __device__ constexpr uint32_t table_slot_bytes(uint32_t k, uint32_t w) {
   return (k * table_bytes_per_input(w) + 255u) & ~255u;
 }
 
-// Decode tuning switches (DecodeParams::flags), read from the environment at
-// each launch so that tools/ab_bench.py can compare them in one process:
-// ECAMD_DEC_PLAIN_STORES=1 / ECAMD_DEC_CACHED_LOADS=1 switch decode's output
-// stores / input loads from nontemporal to the default cache policy.
-// ECAMD_DEC_REALIGN=1 stores decode's object slices as lane-shifted aligned
-// 16-B units instead of plain (misaligned) 16-B lane stores; measured slower
-// on MI355X, so off by default.
-// ECAMD_XCD=0 turns off the XCD-contiguous work split (every kernel).
-constexpr uint32_t kFlagPlainStores = 1u;
-constexpr uint32_t kFlagCachedLoads = 2u;
-constexpr uint32_t kFlagNoRealign = 4u;
+// ECAMD_XCD=0 turns off the XCD-major work split (every kernel).
 
 struct EncodeParams {
   const uint8_t* objs;      // object o at objs + o * obj_stride
@@ -64,8 +55,8 @@ struct EncodeParams {
   uint32_t row0, nrows;     // parity rows handled by this pass
   uint32_t bs;              // payload bytes per fragment
   uint32_t n_obj;
-  uint32_t tiles, first_edge;  // set by the launcher (split_tiles)
-  uint32_t xcd_split;          // set by the launcher (item_range)
+  uint32_t chunks, edge_chunks;  // set by the launcher (split_chunks)
+  uint32_t xcd_split;            // set by the launcher (global_wave)
 };
 
 // Per-object decode / reconstruct descriptor (device memory).
@@ -98,24 +89,16 @@ struct DecodeParams {
   uint32_t reconstruct;     // 1 = write fragment payload + header
   uint32_t compact;         // 1 = input c of object o at frags + o*stripe_stride
                             //     + c*frag_stride (only the k inputs are present)
-  uint32_t tiles, first_edge;  // set by the launcher (split_tiles)
-  uint32_t xcd_split;          // set by the launcher (item_range)
-  uint32_t flags;              // set by the launcher (kFlag*)
+  uint32_t mode;            // kernel variant (ec_kernels_impl.hpp DecodeMode): 0 = decode
+                            // with every missing row in this pass, 1 = reconstruct,
+                            // 2 = generic (multi-pass decode)
+  uint32_t chunks, edge_chunks;  // set by the launcher (split_chunks)
+  uint32_t xcd_split;            // set by the launcher (global_wave)
 };
 
-// Dispatch on p.w.
+// Dispatch on (p.w, p.k) to the per-k instantiations (ec_dispatch.cpp).
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);
 hipError_t launch_decode(const DecodeParams& p, hipStream_t stream);
-// Per-field instantiations (ec_gf16.hip, ec_gf8.hip).
-hipError_t launch_encode_gf16(const EncodeParams& p, hipStream_t stream);
-hipError_t launch_decode_gf16(const DecodeParams& p, hipStream_t stream);
-hipError_t launch_encode_gf8(const EncodeParams& p, hipStream_t stream);
-hipError_t launch_decode_gf8(const DecodeParams& p, hipStream_t stream);
 
-// Number of 256-chunk tiles per fragment payload.
-inline uint32_t tiles_per_fragment(uint32_t bs) {
-  const uint32_t chunks = (bs + 15) / 16;
-  return (chunks + kThreadsPerBlock - 1) / kThreadsPerBlock;
-}
 
 }  // namespace ecamd

@@ -31,12 +31,14 @@
 // Memory.  Each lane moves 16 B per input per step (global_load_dwordx4,
 // 1 KiB contiguous per wave-instruction); inputs are read once from HBM and
 // every output byte is written once.  Fragment payloads inside an object
-// start at j*bs, which is only 2-byte (GF(2^16)) or 1-byte aligned; the loads
-// rely on gfx9's unaligned-access mode for those inputs.
+// start at j*bs, which is only 2-byte (GF(2^16)) or 1-byte aligned: encode
+// reads those slices with gfx9's unaligned loads; decode writes them as
+// realigned 16-B units (see "Realigned object stores").
 #pragma once
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 #include <mutex>
 #include <unordered_map>
 
@@ -80,6 +82,34 @@ __device__ __forceinline__ void st_stream(void* p, const uint4& x) {
   v.z = x.z;
   v.w = x.w;
   __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
+}
+
+// Buffer access to the interior streams: a wave-uniform descriptor per
+// object (base made provably uniform with readfirstlane, so hipcc builds it
+// in SGPRs without a waterfall loop: cdna_hip_programming.md T20), the lane's
+// 16*lane in voffset and every per-input / per-output offset in soffset, so
+// all K loads and stores of a chunk share ONE address VGPR instead of a
+// 64-bit address pair each.  aux 2 = nt (streamed once).
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+constexpr int kNt = 2;
+__device__ __forceinline__ Rsrc rsrc(const void* base) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, -1, 0x00020000);
+}
+__device__ __forceinline__ uint4 buf_ld(Rsrc r, uint32_t voff, uint32_t soff) {
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kNt);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void buf_st(Rsrc r, uint32_t voff, uint32_t soff, const uint4& x) {
+  v4u v;
+  v.x = x.x;
+  v.y = x.y;
+  v.z = x.z;
+  v.w = x.w;
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, kNt);
 }
 
 // a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
@@ -218,6 +248,15 @@ struct Gf8 {
 
 // ---------------- common helpers ----------------
 
+constexpr uint32_t kLanes = 64;
+constexpr uint32_t kChunkBytes = kLanes * 16;  // one 16-B-per-lane wave access
+constexpr uint32_t kWavesPerBlock = kThreadsPerBlock / kLanes;
+
+__device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & (kLanes - 1); }
+__device__ __forceinline__ uint32_t wave_in_block() {
+  return __builtin_amdgcn_readfirstlane(threadIdx.x / kLanes);
+}
+
 // 16 bytes at base+off; bytes at or past `len` read as zero (encode padding).
 __device__ __forceinline__ uint4 load_clamped(const uint8_t* base, uint64_t off, uint64_t len) {
   if (off + 16 <= len) return *reinterpret_cast<const uint4*>(base + off);
@@ -227,25 +266,37 @@ __device__ __forceinline__ uint4 load_clamped(const uint8_t* base, uint64_t off,
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+__device__ __forceinline__ uint32_t byte_of(const uint4& v, uint32_t b) {
+  const uint64_t lo = v.x | (static_cast<uint64_t>(v.y) << 32);
+  const uint64_t hi = v.z | (static_cast<uint64_t>(v.w) << 32);
+  return static_cast<uint32_t>((b < 8 ? lo >> (8 * b) : hi >> (8 * (b - 8))) & 0xFFu);
+}
+
+// Bytes [from, from + n) of v stored at p (byte stores; run ends only).
+__device__ __forceinline__ void put_bytes(uint8_t* p, const uint4& v, uint32_t from, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) p[i] = static_cast<uint8_t>(byte_of(v, from + i));
+}
+
 // Store the first `n` (> 0) bytes of v at dst.
 __device__ __forceinline__ void store_partial(uint8_t* dst, const uint4& v, int64_t n) {
   if (n >= 16) {
     *reinterpret_cast<uint4*>(dst) = v;
     return;
   }
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  for (int64_t i = 0; i < n; ++i) dst[i] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
+  put_bytes(dst, v, 0, static_cast<uint32_t>(n));
 }
 
+// One wave writes `count` 80-byte headers (fragment f at frag0 + f*stride).
 __device__ __forceinline__ void copy_headers(uint8_t* frag0, uint64_t stride, const uint8_t* hdr,
                                              uint32_t count) {
-  for (uint32_t i = threadIdx.x; i < count * 5; i += blockDim.x) {
+  for (uint32_t i = lane_id(); i < count * 5; i += kLanes) {
     const uint32_t f = i / 5, part = i - f * 5;
     reinterpret_cast<uint4*>(frag0 + f * stride)[part] =
         reinterpret_cast<const uint4*>(hdr + f * kHeaderBytes)[part];
   }
 }
 
+// Whole block copies `bytes` of tables from global memory to LDS byte `dst`.
 __device__ __forceinline__ void load_tables(const uint32_t* src, uint32_t bytes, uint32_t dst) {
   auto* d = lds_v4(dst);
   const v4u* s = reinterpret_cast<const v4u*>(src);
@@ -264,100 +315,87 @@ __device__ __forceinline__ int64_t object_bytes(uint32_t idx, uint32_t bs, uint3
 
 // ---------------- work decomposition ----------------
 //
-// Work item = (object o, tile of 256 lane chunks = 4 KiB of payload
-// positions).  Tiles [0, first_edge) of every object are "interior": all
-// lanes read 16 in-bounds bytes from every input and write 16 bytes to every
-// output, so they run with no bounds checks, unrolled over K and with the
-// next item's loads in flight (register double buffering).  Tiles
-// [first_edge, tiles) -- at most two per object: the payload tail and the
-// tile reaching the zero padding / the end of the object -- are "edge" items
-// with per-lane bounds; each block takes its share of them before entering
-// the interior loop, all K loads of an edge item in flight at once.
+// Chunk = 1 KiB of payload positions of one object (64 lanes x 16 B): one
+// wave-instruction per input and per output.  Chunks [0, chunks) of every
+// fragment are "interior": every lane reads 16 in-bounds bytes from every
+// input and writes 16 bytes to every output, so they run with no bounds
+// checks.  The flattened interior space (object-major) is cut into one
+// contiguous range per wave, balanced to +-1 chunk, and each wave walks its
+// range in order.  So consecutive chunks of a fragment are read (encode: the
+// unaligned object slices) and written (decode: the unaligned object slices)
+// by ONE wave back to back: the 128-B lines two chunks share are fetched once
+// and written whole, and no other CU ever touches them.  Chunks [chunks,
+// chunks + edge_chunks) -- at most two per object: the payload tail and the
+// chunk reaching the zero padding / the end of the object -- are "edge" items
+// with per-lane bounds, dealt to the waves from the other end of the grid.
+//
+// XCD placement (speed only): workgroups are dealt round-robin over the 8
+// XCDs (MI355X_MICROARCH.md), so with xcd_split the range index is made
+// XCD-major -- the waves of one XCD own one contiguous eighth of the space,
+// and the few lines shared at range boundaries stay inside one L2.
 
-__device__ __forceinline__ void tile_of(uint32_t w, uint32_t per_obj, uint32_t first,
-                                        uint32_t& o, uint32_t& tile, uint32_t& t) {
-  o = w / per_obj;
-  tile = first + (w - o * per_obj);
-  t = (tile * kThreadsPerBlock + threadIdx.x) << 4;
+__device__ __forceinline__ uint32_t global_wave(uint32_t xcd_split) {
+  uint32_t b = blockIdx.x;
+  if (xcd_split) b = (b & 7u) * (gridDim.x >> 3) + (b >> 3);
+  return b * kWavesPerBlock + wave_in_block();
 }
 
-// Interior item ranges.  Blocks are dealt round-robin over the 8 XCDs (blocks
-// b and b+8 share one; MI355X_MICROARCH.md), each XCD with its own L2.  With
-// xcd_split the item list is cut into 8 contiguous ranges and range x is
-// walked, grid-stride, by the blocks with b % 8 == x: neighbouring tiles of a
-// fragment then run on one XCD at about the same time, so the 128-B lines
-// they share -- the unaligned object slices that encode reads and decode
-// writes -- meet in one L2 instead of being fetched twice or written back as
-// two partial lines.  Placement only changes speed, never results.
-struct ItemRange {
-  uint32_t begin, end, step;
+struct Range {
+  uint32_t begin, end;
 };
-__device__ __forceinline__ ItemRange item_range(uint32_t items, uint32_t xcd_split) {
-  if (!xcd_split) return {blockIdx.x, items, gridDim.x};
-  const uint32_t x = blockIdx.x & 7u;
-  const uint32_t lo = static_cast<uint32_t>(static_cast<uint64_t>(items) * x / 8);
-  const uint32_t hi = static_cast<uint32_t>(static_cast<uint64_t>(items) * (x + 1) / 8);
-  return {lo + (blockIdx.x >> 3), hi, gridDim.x >> 3};
+__device__ __forceinline__ Range wave_range(uint32_t total, uint32_t g) {
+  const uint64_t waves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+  return {static_cast<uint32_t>(static_cast<uint64_t>(total) * g / waves),
+          static_cast<uint32_t>(static_cast<uint64_t>(total) * (g + 1) / waves)};
+}
+
+__device__ __forceinline__ void next_chunk(uint32_t chunks, uint32_t& o, uint32_t& c) {
+  if (++c == chunks) {
+    c = 0;
+    ++o;
+  }
 }
 
 // ---------------- encode ----------------
 
-__device__ __forceinline__ void encode_headers(const EncodeParams& p, uint32_t o, uint32_t k) {
-  if (p.headers == nullptr) return;
-  if (p.row0 == 0)
-    copy_headers(p.parity + static_cast<uint64_t>(o) * p.stripe_stride, p.frag_stride,
-                 p.headers + k * kHeaderBytes, p.m);
-  if (p.data != nullptr)
-    copy_headers(p.data + static_cast<uint64_t>(o) * p.stripe_stride, p.frag_stride, p.headers,
-                 k);
-}
-
 template <int K>
-__device__ __forceinline__ void encode_load(const EncodeParams& p, uint32_t o, uint32_t t,
+__device__ __forceinline__ void encode_load(const EncodeParams& p, uint32_t o, uint32_t c,
                                             uint4 (&x)[K]) {
-  const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride + t;
+  const Rsrc r = rsrc(p.objs + static_cast<uint64_t>(o) * p.obj_stride);
 #pragma unroll
-  for (int j = 0; j < K; ++j) x[j] = ld_stream(obj + static_cast<uint64_t>(j) * p.bs);
+  for (int j = 0; j < K; ++j) x[j] = buf_ld(r, lane_id() * 16, j * p.bs + c * kChunkBytes);
 }
 
-// One interior item with its inputs in `cur`.  PREFETCH: first issue the
-// loads of the block's next item (w + step) into `nxt`, so they are in flight
-// while this item's table lookups run.
-//
-// Every memory operation in here is unconditional (NR output rows, no
-// headers, no data copies) so that hipcc's s_waitcnt insertion sees one
-// sequence per item: before using cur[j] it then waits only for cur's own
-// loads (vmcnt = the ops issued after them), not for the prefetch.  A branch
-// around any load or store in the loop body makes it fall back to the
-// shortest path's count -- measured as vmcnt(9) before cur[0], i.e. waiting
-// for the next item's loads too, which serialised memory and compute.
-template <class F, int K, int NR, bool PREFETCH>
-__device__ __forceinline__ void encode_item(const EncodeParams& p, uint32_t w, uint32_t step,
-                                            uint4 (&cur)[K], uint4 (&nxt)[K]) {
-  uint32_t o, tile, t;
-  tile_of(w, p.first_edge, 0, o, tile, t);
-  if constexpr (PREFETCH) {
-    uint32_t on, tn, ttn;
-    tile_of(w + step, p.first_edge, 0, on, tn, ttn);
-    encode_load<K>(p, on, ttn, nxt);
-  }
+// One interior chunk with its inputs in `cur`; first issues the loads of the
+// wave's next chunk (on, cn) into `nxt` so they are in flight during the
+// table lookups.  The last chunk of a range "prefetches" itself again (an L2
+// hit): every memory operation in the loop body is unconditional, so hipcc's
+// s_waitcnt before cur[j] waits only for cur's own loads (a branch around a
+// load or store makes it fall back to the shortest path's count, measured in
+// round 1 as waiting for the prefetch too).
+template <class F, int K, int NR>
+__device__ __forceinline__ void encode_item(const EncodeParams& p, uint32_t o, uint32_t c,
+                                            uint32_t on, uint32_t cn, uint4 (&cur)[K],
+                                            uint4 (&nxt)[K]) {
+  encode_load<K>(p, on, cn, nxt);
   typename F::Acc s;
   F::zero(s);
 #pragma unroll
   for (int j = 0; j < K; ++j) F::mac(F::kb(0), j * F::kTableBytes, cur[j], s);
   F::pin(s);
-  uint8_t* par = p.parity + static_cast<uint64_t>(o) * p.stripe_stride + p.row0 * p.frag_stride +
-                 kHeaderBytes + t;
+  const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
+  const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + c * kChunkBytes;
 #pragma unroll
-  for (int q = 0; q < NR; ++q) st_stream(par + q * p.frag_stride, F::row(s, q));
+  for (int q = 0; q < NR; ++q) buf_st(par, lane_id() * 16, soff + q * p.frag_stride, F::row(s, q));
 }
 
-// Edge item: payload tail (t + 16 > bs) and chunks reaching the zero padding
+// Edge chunk: payload tail (t + 16 > bs) and chunks reaching the zero padding
 // past obj_len (liberasurecode's prepare_fragments_for_encode zero-fills).
 template <class F, int K, int NR>
 __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t e) {
-  uint32_t o, tile, t;
-  tile_of(e, p.tiles - p.first_edge, p.first_edge, o, tile, t);
+  const uint32_t o = e / p.edge_chunks;
+  const uint32_t c = p.chunks + (e - o * p.edge_chunks);
+  const uint32_t t = c * kChunkBytes + lane_id() * 16;
   if (t >= p.bs) return;
   const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride;
   const int64_t rem = static_cast<int64_t>(p.bs) - t;
@@ -378,49 +416,51 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
 template <class F, int K, int NR>
 __global__ void __launch_bounds__(kThreadsPerBlock) encode_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
-  if (p.headers != nullptr)
-    for (uint32_t o = blockIdx.x; o < p.n_obj; o += gridDim.x) encode_headers(p, o, K);
+  const uint32_t g = global_wave(p.xcd_split);
+  const uint32_t G = gridDim.x * kWavesPerBlock;
+  if (p.headers != nullptr && p.row0 == 0)
+    for (uint32_t o = g; o < p.n_obj; o += G) {
+      const uint64_t base = static_cast<uint64_t>(o) * p.stripe_stride;
+      copy_headers(p.parity + base, p.frag_stride, p.headers + K * kHeaderBytes, p.m);
+      if (p.data != nullptr) copy_headers(p.data + base, p.frag_stride, p.headers, K);
+    }
   __syncthreads();
-  const ItemRange r = item_range(p.n_obj * p.first_edge, p.xcd_split);
-  uint4 xa[K], xb[K];
-  uint32_t w = r.begin;
-  if (w < r.end) {
-    uint32_t o, tile, t;
-    tile_of(w, p.first_edge, 0, o, tile, t);
-    encode_load<K>(p, o, t, xa);
-    // two items per trip so cur / nxt stay compile-time register arrays;
-    // the last item of the range runs without a prefetch
+  const Range r = wave_range(p.n_obj * p.chunks, g);
+  if (r.begin < r.end) {
+    uint4 xa[K], xb[K];
+    uint32_t i = r.begin;
+    uint32_t o = i / p.chunks, c = i - o * p.chunks;
+    encode_load<K>(p, o, c, xa);
+    // two chunks per trip so cur / nxt stay compile-time register arrays
     while (true) {
-      if (w + r.step >= r.end) {
-        encode_item<F, K, NR, false>(p, w, r.step, xa, xb);
-        break;
-      }
-      encode_item<F, K, NR, true>(p, w, r.step, xa, xb);
-      w += r.step;
-      if (w + r.step >= r.end) {
-        encode_item<F, K, NR, false>(p, w, r.step, xb, xa);
-        break;
-      }
-      encode_item<F, K, NR, true>(p, w, r.step, xb, xa);
-      w += r.step;
+      uint32_t on = o, cn = c;
+      if (i + 1 < r.end) next_chunk(p.chunks, on, cn);
+      encode_item<F, K, NR>(p, o, c, on, cn, xa, xb);
+      if (++i >= r.end) break;
+      o = on;
+      c = cn;
+      if (i + 1 < r.end) next_chunk(p.chunks, on, cn);
+      encode_item<F, K, NR>(p, o, c, on, cn, xb, xa);
+      if (++i >= r.end) break;
+      o = on;
+      c = cn;
     }
   }
-  // edge items last, on the highest-numbered blocks (those with the fewest
-  // interior items)
-  const uint32_t n_edge = p.n_obj * (p.tiles - p.first_edge);
-  for (uint32_t e = gridDim.x - 1 - blockIdx.x; e < n_edge; e += gridDim.x)
-    encode_edge_item<F, K, NR>(p, e);
+  const uint32_t n_edge = p.n_obj * p.edge_chunks;
+  for (uint32_t e = G - 1 - g; e < n_edge; e += G) encode_edge_item<F, K, NR>(p, e);
 }
 
 // Data fragments (optional output of encode): the k padded object slices
-// copied into their fragment payloads.  Item = (object, fragment, 4 KiB tile).
+// copied into their fragment payloads, one wave per (object, fragment, chunk).
 __global__ void __launch_bounds__(kThreadsPerBlock) copy_data_kernel(EncodeParams p) {
-  const uint32_t per_obj = p.k * p.tiles;
+  const uint32_t per_frag = p.chunks + p.edge_chunks;
+  const uint32_t per_obj = p.k * per_frag;
   const uint32_t items = p.n_obj * per_obj;
-  for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
+  const uint32_t G = gridDim.x * kWavesPerBlock;
+  for (uint32_t w = blockIdx.x * kWavesPerBlock + wave_in_block(); w < items; w += G) {
     const uint32_t o = w / per_obj, rest = w - o * per_obj;
-    const uint32_t j = rest / p.tiles, tile = rest - j * p.tiles;
-    const uint32_t t = (tile * kThreadsPerBlock + threadIdx.x) << 4;
+    const uint32_t j = rest / per_frag, c = rest - j * per_frag;
+    const uint32_t t = c * kChunkBytes + lane_id() * 16;
     if (t >= p.bs) continue;
     const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride;
     const uint4 x = load_clamped(obj, static_cast<uint64_t>(j) * p.bs + t, p.obj_len);
@@ -433,268 +473,299 @@ __global__ void __launch_bounds__(kThreadsPerBlock) copy_data_kernel(EncodeParam
 // ---------------- decode / reconstruct ----------------
 //
 // Table sets.  Each object's descriptor names a table set (its erasure
-// pattern's decode rows); consecutive items of a block usually belong to
-// different objects.  LDS holds two slots: a new set goes into the slot not
-// in use, so one barrier per change suffices -- a wave writes slot s only
-// after passing the barrier of the previous change, which every wave reaches
-// only after finishing the items that read slot s.  The interior loop fetches
-// the next item's set into registers together with its payload loads, so a
-// change costs a few ds_writes and one barrier, not an L2 round trip.
+// pattern's decode rows).  Every wave owns one LDS slot and loads a set into
+// it when its run moves to an object with a different pattern -- no
+// workgroup barrier, since a wave's LDS operations execute in order.
+//
+// Realigned object stores.  Decode writes data slice j of an object at
+// j*bs + t, and bs is rarely a multiple of 16 (419,432 = 8 mod 16 at 4 MiB,
+// k = 10), so a plain 16-B lane store would straddle two 16-B units (the
+// memory pipeline splits it in two, and the lines at both ends of every wave
+// access are written as partial lines).  The shift s = (j*bs) mod 16 is
+// uniform over the slice, so each lane instead stores the aligned unit that
+// starts s bytes below its own address: the last s bytes of lane L-1's data
+// (DPP wave_shr:1) and its own first 16 - s bytes.  Lane 0 takes its s bytes
+// from lane 63 of the wave's previous chunk of the same slice, kept in SGPRs
+// (`carry`, v_readlane) -- so along a run every store is one aligned
+// dwordx4, and only the first chunk's lane 0 (head) and the run's last s
+// bytes (tail) are written piecewise.
 
-struct Slots {
-  uint32_t table;  // set in the current slot (0xFFFFFFFF = none)
-  uint32_t slot;   // 0 / 1
+// Carries live in four VGPRs, one per dword: lane i of cw[w] holds dword w of
+// slot i's carry (slot = the store's position in the item: input / row).
+struct Carry {
+  uint32_t w[4];
 };
-
-template <class F, int K>
-struct TablePre {
-  static constexpr int kChunks = K * F::kTableBytes / 16;
-  static constexpr int kPer = (kChunks + kThreadsPerBlock - 1) / kThreadsPerBlock;
-  uint4 v[kPer];
-  uint32_t table;
-};
-
-template <class F, int K>
-__device__ __forceinline__ void table_prefetch(const DecodeParams& p, uint32_t table,
-                                               TablePre<F, K>& pre) {
-  const uint4* src = reinterpret_cast<const uint4*>(
-      p.tables + static_cast<uint64_t>(table) * (K * F::kTableBytes / 4));
-#pragma unroll
-  for (int i = 0; i < TablePre<F, K>::kPer; ++i) {
-    const uint32_t c = threadIdx.x + i * kThreadsPerBlock;
-    if (c < static_cast<uint32_t>(TablePre<F, K>::kChunks)) pre.v[i] = src[c];
-  }
-  pre.table = table;
+// v with lane LANE replaced by the uniform value x (v_writelane_b32; hipcc
+// has no builtin for it).  The lane select is an inline constant: with an
+// SGPR it would be the instruction's second constant-bus read.
+template <int LANE>
+__device__ __forceinline__ uint32_t writelane(uint32_t v, uint32_t x) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(x), "i"(LANE));
+  return v;
 }
 
-// Make d's table set current; returns its kb.  Block-uniform (barrier).
-template <class F, int K>
-__device__ __forceinline__ uint32_t ensure_tables(const DecodeParams& p, const ObjDesc& d,
-                                                  Slots& st, const TablePre<F, K>& pre) {
-  constexpr uint32_t kSlot = table_slot_bytes(K, F::kW);
-  if (d.n_out != 0 && d.table != st.table) {
-    st.slot ^= 1u;
-    const uint32_t base = st.slot * kSlot;
-    if (pre.table == d.table) {
-      auto* dst = lds_v4(base);
-#pragma unroll
-      for (int i = 0; i < TablePre<F, K>::kPer; ++i) {
-        const uint32_t c = threadIdx.x + i * kThreadsPerBlock;
-        if (c < static_cast<uint32_t>(TablePre<F, K>::kChunks)) {
-          v4u v;
-          v.x = pre.v[i].x;
-          v.y = pre.v[i].y;
-          v.z = pre.v[i].z;
-          v.w = pre.v[i].w;
-          dst[c] = v;
-        }
-      }
-    } else {
-      load_tables(p.tables + static_cast<uint64_t>(d.table) * (K * F::kTableBytes / 4),
-                  K * F::kTableBytes, base);
+// f(std::integral_constant<int, I>) for I = 0 .. N-1, each I a compile-time
+// constant (the carry slot of a store must be one).
+template <int I, int N, class Fn>
+__device__ __forceinline__ void static_for(Fn&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, N>(f);
+  }
+}
+__device__ __forceinline__ uint32_t shr1(uint32_t v, uint32_t old) {
+  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(
+      static_cast<int>(old), static_cast<int>(v), 0x138 /* wave_shr:1 */, 0xF, 0xF, false));
+}
+
+// Store a lane's 16 B `v` for `dst` (dst mod 16 == s, uniform) of one chunk
+// of a run: the unit at dst - s = last s bytes of lane L-1's v (lane 0: the
+// carried lane 63 of the previous chunk) + first 16 - s bytes of its own.
+// Only the dwords of the previous lane that the unit uses are moved (dword
+// offset d = (16 - s) / 4).  FIRST: the run's first chunk (no carry yet:
+// lane 0 writes only its own bytes).  Every path issues exactly one vector
+// store instruction, so the s_waitcnt counts hipcc derives stay exact.
+// (The destination is out + soff + 16*lane; outp is `out` as a pointer.)
+template <bool FIRST, int SLOT>
+__device__ __forceinline__ void st_slice(Rsrc out, uint8_t* outp, uint32_t soff, const uint4& v,
+                                         uint32_t s, Carry& cw) {
+  if (s == 0) {
+    buf_st(out, lane_id() * 16, soff, v);
+    return;
+  }
+  const uint32_t st = 16u - s, r = st & 3u;
+  uint4 u;
+  const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+  // pv_i = dword i of lane L-1's v (lane 0: carry); update the carry with
+  // lane 63's dword i for the next chunk
+#define ECAMD_PV(i)                                                                 \
+  const uint32_t pv##i = shr1(vv[i], __builtin_amdgcn_readlane(cw.w[i], SLOT));     \
+  cw.w[i] = writelane<SLOT>(cw.w[i], __builtin_amdgcn_readlane(vv[i], 63));
+  switch (st >> 2) {
+    case 0: {
+      ECAMD_PV(0) ECAMD_PV(1) ECAMD_PV(2) ECAMD_PV(3)
+      u = make_uint4(__builtin_amdgcn_alignbyte(pv1, pv0, r), __builtin_amdgcn_alignbyte(pv2, pv1, r),
+                     __builtin_amdgcn_alignbyte(pv3, pv2, r), __builtin_amdgcn_alignbyte(v.x, pv3, r));
+      break;
     }
-    __syncthreads();
-    st.table = d.table;
+    case 1: {
+      ECAMD_PV(1) ECAMD_PV(2) ECAMD_PV(3)
+      u = make_uint4(__builtin_amdgcn_alignbyte(pv2, pv1, r), __builtin_amdgcn_alignbyte(pv3, pv2, r),
+                     __builtin_amdgcn_alignbyte(v.x, pv3, r), __builtin_amdgcn_alignbyte(v.y, v.x, r));
+      break;
+    }
+    case 2: {
+      ECAMD_PV(2) ECAMD_PV(3)
+      u = make_uint4(__builtin_amdgcn_alignbyte(pv3, pv2, r), __builtin_amdgcn_alignbyte(v.x, pv3, r),
+                     __builtin_amdgcn_alignbyte(v.y, v.x, r), __builtin_amdgcn_alignbyte(v.z, v.y, r));
+      break;
+    }
+    default: {
+      ECAMD_PV(3)
+      u = make_uint4(__builtin_amdgcn_alignbyte(v.x, pv3, r), __builtin_amdgcn_alignbyte(v.y, v.x, r),
+                     __builtin_amdgcn_alignbyte(v.z, v.y, r), __builtin_amdgcn_alignbyte(v.w, v.z, r));
+      break;
+    }
   }
-  return F::kb(st.slot * kSlot);
+#undef ECAMD_PV
+  if (FIRST && lane_id() == 0)
+    put_bytes(outp + soff, v, 0, 16 - s);
+  else
+    buf_st(out, lane_id() * 16, soff - s, u);
 }
 
-__device__ __forceinline__ void reconstruct_header(const DecodeParams& p, const ObjDesc& d,
-                                                   uint8_t* out) {
-  if (threadIdx.x < 5)
-    reinterpret_cast<uint4*>(out)[threadIdx.x] = reinterpret_cast<const uint4*>(
-        p.headers + static_cast<uint64_t>(d.header) * kHeaderBytes)[threadIdx.x];
+// After a run: bytes [end - s, end) of the slice are the last s bytes of the
+// final chunk's lane 63, i.e. dwords of the carry.
+__device__ __forceinline__ void st_slice_tail(uint8_t* end, uint32_t s, const Carry& cw,
+                                              int slot) {
+  if (s == 0) return;
+  const uint4 c = make_uint4(__builtin_amdgcn_readlane(cw.w[0], slot),
+                             __builtin_amdgcn_readlane(cw.w[1], slot),
+                             __builtin_amdgcn_readlane(cw.w[2], slot),
+                             __builtin_amdgcn_readlane(cw.w[3], slot));
+  if (lane_id() == 0) put_bytes(end - s, c, 16 - s, s);
 }
 
-// Position of input c inside the object's fragment group.
+// Make the table set current in this wave's LDS slot; returns its kb.
+template <class F, int K>
+__device__ __forceinline__ uint32_t wave_tables(const DecodeParams& p, uint32_t table,
+                                                uint32_t& cur) {
+  constexpr uint32_t kSlot = table_slot_bytes(K, F::kW);
+  const uint32_t base = wave_in_block() * kSlot;
+  if (table != cur) {
+    const v4u* src =
+        reinterpret_cast<const v4u*>(p.tables + static_cast<uint64_t>(table) * (K * F::kTableBytes / 4));
+    auto* dst = lds_v4(base);
+    for (uint32_t i = lane_id(); i < K * F::kTableBytes / 16; i += kLanes) dst[i] = src[i];
+    cur = table;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+  return F::kb(base);
+}
+
+// Fragment group position of input c.
 __device__ __forceinline__ uint32_t in_pos(const DecodeParams& p, const ObjDesc& d, int c) {
   return p.compact ? static_cast<uint32_t>(c) : d.in_idx[c];
 }
 
 template <int K>
-__device__ __forceinline__ void decode_load(const DecodeParams& p, uint32_t o, uint32_t t,
-                                            uint4 (&x)[K]) {
-  const ObjDesc& d = p.desc[o];
-  const uint8_t* frags = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
-  if (p.flags & kFlagCachedLoads) {
+__device__ __forceinline__ void decode_load(const DecodeParams& p, const ObjDesc& d, Rsrc in,
+                                            uint32_t c, uint4 (&x)[K]) {
 #pragma unroll
-    for (int j = 0; j < K; ++j)
-      x[j] = *reinterpret_cast<const uint4*>(frags + in_pos(p, d, j) * p.frag_stride);
-  } else {
-#pragma unroll
-    for (int j = 0; j < K; ++j) x[j] = ld_stream(frags + in_pos(p, d, j) * p.frag_stride);
-  }
+  for (int j = 0; j < K; ++j)
+    x[j] = buf_ld(in, lane_id() * 16, in_pos(p, d, j) * p.frag_stride + kHeaderBytes + c * kChunkBytes);
 }
 
-__device__ __forceinline__ void st_out(uint8_t* dst, const uint4& v, uint32_t flags) {
-  if (flags & kFlagPlainStores)
-    *reinterpret_cast<uint4*>(dst) = v;
-  else
-    st_stream(dst, v);
+enum DecodeMode : int {
+  kDecode = 0,       // pass 0 and every missing row in it: all k data slices stored
+  kReconstruct = 1,  // one fragment per object (aligned payload)
+  kDecodeGeneric = 2 // other passes (more than 4 missing data fragments)
+};
+
+// Per-run constants, uniform over the wave.
+struct RunCtx {
+  Rsrc in;       // the object's fragment group
+  Rsrc out;      // the object (decode) or output fragment (reconstruct)
+  uint8_t* outp; // same, as a pointer (partial head / tail stores)
+  uint32_t kb;
+  uint32_t e;    // decode: missing data slices computed here
+};
+
+// kDecode: the k inputs are the first k available fragments in ascending
+// order, so the present data fragments come first and the parity inputs --
+// as many as there are missing data slices, e -- are the last e.  After the
+// products, row q overwrites parity input K-e+q: cur[c] then holds data slice
+// slice_of(c) for every c, and all K slices are stored unconditionally.
+__device__ __forceinline__ uint32_t slice_of(const ObjDesc& d, uint32_t e, int K, int c) {
+  return c < K - static_cast<int>(e) ? d.in_idx[c] : d.out_idx[c - (K - static_cast<int>(e))];
 }
 
-// Realigned object stores.  Decode writes data slice j of an object at
-// j*bs + t, and bs is rarely a multiple of 16 (419,432 = 8 mod 16 at 4 MiB,
-// k = 10), so a plain 16-B store per lane straddles two 16-B units and the
-// memory pipeline splits every one of them.  The 64 lanes of an interior
-// item hold one contiguous 1 KiB run, and the misalignment S = dst mod 16 is
-// the same for all of them.  Each lane takes the last S bytes of lane - 1
-// (ds_bpermute) and stores the aligned 16-B unit that begins S bytes before
-// its own address; lane 0 writes the head (its first 16 - S bytes) and
-// lane 63 the tail (its last S bytes) with naturally aligned 8/4/2/1-B
-// stores.  Neighbouring waves' head and tail share one 16-B unit, disjoint
-// bytes.  Requires all 64 lanes active with consecutive 16-B addresses.
-
-// Bytes [FROM, FROM + N) of v stored at p, where p mod 16 == AMOD: the largest
-// naturally aligned piece each time.
-template <int FROM, int N, int AMOD>
-__device__ __forceinline__ void put_bytes(uint8_t* p, const uint4& v) {
-  if constexpr (N > 0) {
-    constexpr int sz = (AMOD % 8 == 0 && N >= 8)   ? 8
-                       : (AMOD % 4 == 0 && N >= 4) ? 4
-                       : (AMOD % 2 == 0 && N >= 2) ? 2
-                                                   : 1;
-    const uint64_t lo = v.x | (static_cast<uint64_t>(v.y) << 32);
-    const uint64_t hi = v.z | (static_cast<uint64_t>(v.w) << 32);
-    uint64_t x;
-    if constexpr (FROM == 0)
-      x = lo;
-    else if constexpr (FROM < 8)
-      x = (lo >> (8 * FROM)) | (hi << (64 - 8 * FROM));
-    else if constexpr (FROM == 8)
-      x = hi;
-    else
-      x = hi >> (8 * (FROM - 8));
-    if constexpr (sz == 8)
-      *reinterpret_cast<uint64_t*>(p) = x;
-    else if constexpr (sz == 4)
-      *reinterpret_cast<uint32_t*>(p) = static_cast<uint32_t>(x);
-    else if constexpr (sz == 2)
-      *reinterpret_cast<uint16_t*>(p) = static_cast<uint16_t>(x);
-    else
-      *p = static_cast<uint8_t>(x);
-    put_bytes<FROM + sz, N - sz, (AMOD + sz) % 16>(p + sz, v);
-  }
-}
-
-template <int S>
-__device__ __forceinline__ void st_shifted(uint8_t* dst, const uint4& v, const uint4& prev,
-                                           uint32_t lane, uint32_t flags) {
-  // unit byte b = concat(prev, v)[16 - S + b]
-  constexpr int st = 16 - S, d = st >> 2, r = st & 3;
-  const uint32_t w[8] = {prev.x, prev.y, prev.z, prev.w, v.x, v.y, v.z, v.w};
-  uint32_t c[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if constexpr (r == 0)
-      c[i] = w[d + i];
-    else
-      c[i] = __builtin_amdgcn_alignbyte(w[d + i + 1], w[d + i], r);
-  }
-  uint8_t* unit = dst - S;
-  if (lane != 0)
-    st_out(unit, make_uint4(c[0], c[1], c[2], c[3]), flags);
-  else
-    put_bytes<0, 16 - S, S>(dst, v);
-  if (lane == 63) put_bytes<16 - S, S, 0>(unit + 16, v);
-}
-
-__device__ __forceinline__ void st_object(uint8_t* dst, const uint4& v, uint32_t flags) {
-  const uint32_t s = __builtin_amdgcn_readfirstlane(
-      static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst)) & 15u);
-  if (s == 0 || (flags & kFlagNoRealign)) {
-    st_out(dst, v, flags);
-    return;
-  }
-  const uint4 prev = make_uint4(static_cast<uint32_t>(__shfl_up(static_cast<int>(v.x), 1)),
-                                static_cast<uint32_t>(__shfl_up(static_cast<int>(v.y), 1)),
-                                static_cast<uint32_t>(__shfl_up(static_cast<int>(v.z), 1)),
-                                static_cast<uint32_t>(__shfl_up(static_cast<int>(v.w), 1)));
-  const uint32_t lane = threadIdx.x & 63u;
-  switch (s) {
-#define ECAMD_SHIFT_CASE(S) \
-  case S:                   \
-    st_shifted<S>(dst, v, prev, lane, flags); \
+template <class F, int K>
+__device__ __forceinline__ void place_rows(const typename F::Acc& s, uint32_t e, uint4 (&x)[K]) {
+  constexpr int L = K < 4 ? K : 4;
+  switch (e) {
+#define ECAMD_PLACE(E)                                                    \
+  case E:                                                                 \
+    if constexpr (E <= L) {                                               \
+      _Pragma("unroll") for (int q = 0; q < E; ++q) x[K - E + q] = F::row(s, q); \
+    }                                                                     \
     break;
-    ECAMD_SHIFT_CASE(1) ECAMD_SHIFT_CASE(2) ECAMD_SHIFT_CASE(3) ECAMD_SHIFT_CASE(4)
-    ECAMD_SHIFT_CASE(5) ECAMD_SHIFT_CASE(6) ECAMD_SHIFT_CASE(7) ECAMD_SHIFT_CASE(8)
-    ECAMD_SHIFT_CASE(9) ECAMD_SHIFT_CASE(10) ECAMD_SHIFT_CASE(11) ECAMD_SHIFT_CASE(12)
-    ECAMD_SHIFT_CASE(13) ECAMD_SHIFT_CASE(14) ECAMD_SHIFT_CASE(15)
-#undef ECAMD_SHIFT_CASE
+    ECAMD_PLACE(1) ECAMD_PLACE(2) ECAMD_PLACE(3) ECAMD_PLACE(4)
+#undef ECAMD_PLACE
     default:
       break;
   }
 }
 
-// One interior decode / reconstruct item with inputs in `cur`; prefetches the
-// block's next item (payloads into `nxt`, its table set into `pre`).
-template <class F, int K>
-__device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, const ItemRange& r,
-                                            Slots& st, TablePre<F, K>& pre, uint4 (&cur)[K],
-                                            uint4 (&nxt)[K]) {
-  const uint32_t bs = p.bs;
-  uint32_t o, tile, t;
-  tile_of(w, p.first_edge, 0, o, tile, t);
-  const bool more = w + r.step < r.end;
-  uint32_t on = 0;
-  if (more) {
-    uint32_t tn, ttn;
-    tile_of(w + r.step, p.first_edge, 0, on, tn, ttn);
-    decode_load<K>(p, on, ttn, nxt);
-  }
-  const ObjDesc& d = p.desc[o];
-  const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
-  if (more) {
-    const ObjDesc& dn = p.desc[on];
-    if (dn.n_out != 0 && dn.table != st.table && dn.table != pre.table)
-      table_prefetch<F, K>(p, dn.table, pre);
-  }
-  uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
-  if (p.reconstruct && tile == 0) reconstruct_header(p, d, out);
-  const uint32_t n_out = d.n_out;
-
+template <class F, int K, int MODE, bool FIRST>
+__device__ __forceinline__ void decode_item(const DecodeParams& p, const ObjDesc& d,
+                                            const RunCtx& R, uint32_t c, uint32_t cn,
+                                            uint4 (&cur)[K], uint4 (&nxt)[K], Carry& cw) {
+  decode_load<K>(p, d, R.in, cn, nxt);
+  const uint32_t t = c * kChunkBytes;  // + 16*lane in voffset
   typename F::Acc s;
   F::zero(s);
-  if (n_out != 0) {
+  const uint32_t n_rows = MODE == kDecode ? R.e : d.n_out;
+  if (n_rows != 0) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) F::mac(kb, j * F::kTableBytes, cur[j], s);
+    for (int j = 0; j < K; ++j) F::mac(R.kb, j * F::kTableBytes, cur[j], s);
   }
   F::pin(s);
-
-#pragma unroll
-  for (int q = 0; q < kRowsPerPass; ++q) {
-    if (q >= static_cast<int>(n_out)) break;
-    uint8_t* dst = p.reconstruct ? out + kHeaderBytes + t
-                                 : out + static_cast<uint64_t>(d.out_idx[q]) * bs + t;
-    st_object(dst, F::row(s, q), p.flags);
+  if constexpr (MODE == kDecode) {
+    place_rows<F, K>(s, R.e, cur);
+    static_for<0, K>([&](auto J) {
+      const uint32_t off = slice_of(d, R.e, K, J) * p.bs;
+      st_slice<FIRST, J>(R.out, R.outp, off + t, cur[J], off & 15u, cw);
+    });
+  } else if constexpr (MODE == kReconstruct) {
+    buf_st(R.out, lane_id() * 16, kHeaderBytes + t, F::row(s, 0));
+  } else {
+    if (d.copy_inputs) {
+      static_for<0, K>([&](auto J) {
+        const uint32_t idx = d.in_idx[J];
+        if (idx < static_cast<uint32_t>(K)) {
+          const uint32_t off = idx * p.bs;
+          st_slice<FIRST, J>(R.out, R.outp, off + t, cur[J], off & 15u, cw);
+        }
+      });
+    }
+    static_for<0, kRowsPerPass>([&](auto Q) {
+      if (Q < static_cast<int>(d.n_out)) {
+        const uint32_t off = d.out_idx[Q] * p.bs;
+        st_slice<FIRST, K + Q>(R.out, R.outp, off + t, F::row(s, Q), off & 15u, cw);
+      }
+    });
   }
-  if (d.copy_inputs) {
+}
+
+// Chunks [c0, c1) of object o.
+template <class F, int K, int MODE>
+__device__ __forceinline__ void decode_run(const DecodeParams& p, uint32_t o, uint32_t c0,
+                                           uint32_t c1, uint32_t& cur_table) {
+  const ObjDesc& d = p.desc[o];
+  RunCtx R;
+  R.in = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride);
+  R.outp = p.out + static_cast<uint64_t>(o) * p.out_stride;
+  R.out = rsrc(R.outp);
+  R.e = d.n_out;
+  R.kb = d.n_out != 0 ? wave_tables<F, K>(p, d.table, cur_table) : 0u;
+  uint4 xa[K], xb[K];
+  Carry cw = {{0, 0, 0, 0}};
+  decode_load<K>(p, d, R.in, c0, xa);
+  uint32_t c = c0;
+  decode_item<F, K, MODE, true>(p, d, R, c, c + 1 < c1 ? c + 1 : c, xa, xb, cw);
+  while (++c < c1) {
+    decode_item<F, K, MODE, false>(p, d, R, c, c + 1 < c1 ? c + 1 : c, xb, xa, cw);
+    if (++c >= c1) break;
+    decode_item<F, K, MODE, false>(p, d, R, c, c + 1 < c1 ? c + 1 : c, xa, xb, cw);
+  }
+  if constexpr (MODE != kReconstruct) {
+    uint8_t* end = R.outp + c1 * kChunkBytes;
+    if constexpr (MODE == kDecode) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const uint32_t idx = d.in_idx[j];
-      if (idx < K) st_object(out + static_cast<uint64_t>(idx) * bs + t, cur[j], p.flags);
+      for (int j = 0; j < K; ++j) {
+        const uint32_t off = slice_of(d, R.e, K, j) * p.bs;
+        st_slice_tail(end + off, off & 15u, cw, j);
+      }
+    } else {
+      if (d.copy_inputs) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const uint32_t idx = d.in_idx[j];
+          if (idx < static_cast<uint32_t>(K)) {
+            const uint32_t off = idx * p.bs;
+            st_slice_tail(end + off, off & 15u, cw, j);
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kRowsPerPass; ++q)
+        if (q < static_cast<int>(d.n_out)) {
+          const uint32_t off = d.out_idx[q] * p.bs;
+          st_slice_tail(end + off, off & 15u, cw, K + q);
+        }
     }
   }
 }
 
-// Edge item of decode / reconstruct: payload tail, and (decode) outputs that
-// cross the end of the object.
+// Edge chunk of decode / reconstruct: payload tail, and (decode) outputs
+// that cross the end of the object.  Byte-exact stores.
 template <class F, int K>
-__device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t e, Slots& st,
-                                                 const TablePre<F, K>& pre) {
-  uint32_t o, tile, t;
-  tile_of(e, p.tiles - p.first_edge, p.first_edge, o, tile, t);
+__device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t e,
+                                                 uint32_t& cur_table) {
+  const uint32_t o = e / p.edge_chunks;
+  const uint32_t c = p.chunks + (e - o * p.edge_chunks);
   const ObjDesc& d = p.desc[o];
-  const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
-  uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
-  if (p.reconstruct && tile == 0) reconstruct_header(p, d, out);
+  const uint32_t kb = d.n_out != 0 ? wave_tables<F, K>(p, d.table, cur_table) : 0u;
+  const uint32_t t = c * kChunkBytes + lane_id() * 16;
   if (t >= p.bs) return;
+  uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
   // t < bs and 16 | t, so t + 16 <= round16(bs) <= frag_stride - 80: in bounds
-  const uint8_t* frags = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
+  const uint8_t* in = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
   uint4 x[K];
 #pragma unroll
   for (int j = 0; j < K; ++j)
-    x[j] = *reinterpret_cast<const uint4*>(frags + in_pos(p, d, j) * p.frag_stride);
+    x[j] = *reinterpret_cast<const uint4*>(in + in_pos(p, d, j) * p.frag_stride);
   typename F::Acc s;
   F::zero(s);
   if (d.n_out != 0) {
@@ -722,30 +793,25 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
   }
 }
 
-template <class F, int K>
-__global__ void __launch_bounds__(kThreadsPerBlock) decode_kernel(DecodeParams p) {
-  const ItemRange r = item_range(p.n_obj * p.first_edge, p.xcd_split);
-  Slots st{0xFFFFFFFFu, 1u};
-  TablePre<F, K> pre;
-  pre.table = 0xFFFFFFFFu;
-  uint4 xa[K], xb[K];
-  uint32_t w = r.begin;
-  if (w < r.end) {
-    uint32_t o, tile, t;
-    tile_of(w, p.first_edge, 0, o, tile, t);
-    decode_load<K>(p, o, t, xa);
-    const ObjDesc& d0 = p.desc[o];
-    if (d0.n_out != 0) table_prefetch<F, K>(p, d0.table, pre);
+template <class F, int K, int MODE>
+__global__ void __launch_bounds__(kThreadsPerBlock) __attribute__((amdgpu_waves_per_eu(4)))
+decode_kernel(DecodeParams p) {
+  const uint32_t g = global_wave(p.xcd_split);
+  const uint32_t G = gridDim.x * kWavesPerBlock;
+  if (MODE == kReconstruct && p.headers != nullptr)
+    for (uint32_t o = g; o < p.n_obj; o += G)
+      copy_headers(p.out + static_cast<uint64_t>(o) * p.out_stride, 0,
+                   p.headers + static_cast<uint64_t>(p.desc[o].header) * kHeaderBytes, 1);
+  uint32_t cur_table = 0xFFFFFFFFu;
+  const Range r = wave_range(p.n_obj * p.chunks, g);
+  for (uint32_t i = r.begin; i < r.end;) {
+    const uint32_t o = i / p.chunks, c0 = i - o * p.chunks;
+    const uint32_t c1 = min(p.chunks, c0 + (r.end - i));
+    decode_run<F, K, MODE>(p, o, c0, c1, cur_table);
+    i += c1 - c0;
   }
-  const uint32_t n_edge = p.n_obj * (p.tiles - p.first_edge);
-  for (uint32_t e = blockIdx.x; e < n_edge; e += gridDim.x) decode_edge_item<F, K>(p, e, st, pre);
-  while (w < r.end) {
-    decode_item<F, K>(p, w, r, st, pre, xa, xb);
-    w += r.step;
-    if (w >= r.end) break;
-    decode_item<F, K>(p, w, r, st, pre, xb, xa);
-    w += r.step;
-  }
+  const uint32_t n_edge = p.n_obj * p.edge_chunks;
+  for (uint32_t e = G - 1 - g; e < n_edge; e += G) decode_edge_item<F, K>(p, e, cur_table);
 }
 
 // ---------------- launch ----------------
@@ -756,7 +822,9 @@ inline bool env_flag(const char* name, bool dflt) {
   return v[0] != '0';
 }
 
-inline int grid_for(const void* kernel, size_t lds_bytes, uint32_t items) {
+// Resident workgroups for the kernel (a multiple of 8 when >= 8, so the XCD
+// split is even), capped by the work available.
+inline int grid_for(const void* kernel, size_t lds_bytes, uint32_t wave_items) {
   int dev = 0, cus = 256, per_cu = 4;
   if (hipGetDevice(&dev) == hipSuccess) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
@@ -767,24 +835,27 @@ inline int grid_for(const void* kernel, size_t lds_bytes, uint32_t items) {
       per_cu = b;
   }
   // The occupancy API can report one block per CU more than fits
-  // (MI355X_MICROARCH.md, Residency); a grid-stride kernel must not queue
-  // blocks behind the resident ones, so stay at <= 4 per CU.
+  // (MI355X_MICROARCH.md, Residency); stay at <= 4 per CU.
   per_cu = std::min(per_cu, 4);
   const uint32_t resident = static_cast<uint32_t>(cus * per_cu);
-  return static_cast<int>(items < resident ? (items ? items : 1) : resident);
+  const uint32_t want = std::max<uint32_t>(1, (wave_items + kWavesPerBlock - 1) / kWavesPerBlock);
+  uint32_t grid = std::min(resident, want);
+  if (grid >= 8) grid &= ~7u;
+  return static_cast<int>(grid);
 }
 
-// Interior tiles per object: tiles whose 4 KiB of positions end at or before
-// min(bs, room), where room = payload bytes of the last data fragment that
-// lie inside the object (decode outputs / encode inputs stop there).
-inline void split_tiles(uint32_t bs, uint64_t obj_len, uint32_t k, bool whole_payload,
-                        uint32_t& tiles, uint32_t& first_edge) {
-  tiles = tiles_per_fragment(bs);
+// Interior chunks per fragment: chunks whose 1 KiB of positions end at or
+// before min(bs, room), where room = payload bytes of the last data fragment
+// that lie inside the object (decode outputs / encode inputs stop there).
+inline void split_chunks(uint32_t bs, uint64_t obj_len, uint32_t k, bool whole_payload,
+                         uint32_t& chunks, uint32_t& edge_chunks) {
+  const uint32_t total = (bs + kChunkBytes - 1) / kChunkBytes;
   int64_t room = whole_payload ? static_cast<int64_t>(bs)
                                : static_cast<int64_t>(obj_len) - static_cast<int64_t>(k - 1) * bs;
   if (room > static_cast<int64_t>(bs)) room = bs;
   if (room < 0) room = 0;
-  first_edge = static_cast<uint32_t>(room / (kThreadsPerBlock * 16));
+  chunks = static_cast<uint32_t>(room / kChunkBytes);
+  edge_chunks = total - chunks;
 }
 
 // The kernels address LDS by raw byte offset from 0, which is only valid when
@@ -803,11 +874,11 @@ inline bool lds_starts_at_zero(const void* kern) {
 }
 
 template <typename Kern, typename Params>
-hipError_t launch(Kern kern, Params p, size_t lds, uint32_t items, hipStream_t stream) {
-  if (items == 0) return hipSuccess;
+hipError_t launch(Kern kern, Params p, size_t lds, uint32_t wave_items, hipStream_t stream) {
+  if (wave_items == 0) return hipSuccess;
   const void* k = reinterpret_cast<const void*>(kern);
   if (!lds_starts_at_zero(k)) return hipErrorInvalidKernelFile;
-  const int grid = grid_for(k, lds, items);
+  const int grid = grid_for(k, lds, wave_items);
   p.xcd_split = (grid >= 8 && grid % 8 == 0 && env_flag("ECAMD_XCD", true)) ? 1u : 0u;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreadsPerBlock), lds, stream, p);
   return hipGetLastError();
@@ -815,13 +886,12 @@ hipError_t launch(Kern kern, Params p, size_t lds, uint32_t items, hipStream_t s
 
 template <class F, int K, int NR>
 hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
-  split_tiles(p.bs, p.obj_len, K, false, p.tiles, p.first_edge);
-  const uint32_t interior = p.n_obj * p.first_edge;
-  const uint32_t edge = p.n_obj * (p.tiles - p.first_edge);
-  hipError_t e = launch(encode_kernel<F, K, NR>, p, K * F::kTableBytes,
-                        std::max(std::max(interior, edge), p.headers ? p.n_obj : 0u), stream);
+  split_chunks(p.bs, p.obj_len, K, false, p.chunks, p.edge_chunks);
+  const uint32_t items = std::max(p.n_obj * p.chunks,
+                                  std::max(p.n_obj * p.edge_chunks, p.headers ? p.n_obj : 0u));
+  hipError_t e = launch(encode_kernel<F, K, NR>, p, K * F::kTableBytes, items, stream);
   if (e != hipSuccess || p.data == nullptr || p.row0 != 0) return e;
-  return launch(copy_data_kernel, p, 0, p.n_obj * K * p.tiles, stream);
+  return launch(copy_data_kernel, p, 0, p.n_obj * K * (p.chunks + p.edge_chunks), stream);
 }
 
 template <class F, int K>
@@ -840,21 +910,14 @@ hipError_t launch_encode_rows(const EncodeParams& p, hipStream_t stream) {
   }
 }
 
-template <class F, int K>
-hipError_t launch_decode_k(DecodeParams p, hipStream_t stream) {
-  split_tiles(p.bs, p.obj_len, K, p.reconstruct != 0, p.tiles, p.first_edge);
-  p.flags = (env_flag("ECAMD_DEC_PLAIN_STORES", false) ? kFlagPlainStores : 0u) |
-            (env_flag("ECAMD_DEC_CACHED_LOADS", false) ? kFlagCachedLoads : 0u) |
-            (env_flag("ECAMD_DEC_REALIGN", false) ? 0u : kFlagNoRealign);
-  const uint32_t interior = p.n_obj * p.first_edge;
-  const uint32_t edge = p.n_obj * (p.tiles - p.first_edge);
-  return launch(decode_kernel<F, K>, p, 2 * table_slot_bytes(K, F::kW), std::max(interior, edge),
-                stream);
+template <class F, int K, int MODE>
+hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
+  split_chunks(p.bs, p.obj_len, K, p.reconstruct != 0, p.chunks, p.edge_chunks);
+  const uint32_t items = std::max(p.n_obj * p.chunks,
+                                  std::max(p.n_obj * p.edge_chunks, p.reconstruct ? p.n_obj : 0u));
+  const size_t lds = kWavesPerBlock * table_slot_bytes(K, F::kW);
+  return launch(decode_kernel<F, K, MODE>, p, lds, items, stream);
 }
-
-#define ECAMD_K_CASES(X) \
-  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
-  X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31)
 
 }  // namespace
 }  // namespace ecamd

@@ -641,6 +641,9 @@ hipError_t launch_range(Instance& I, const DecodeJob& J, int o0, int o1, uint32_
     P.n_obj = static_cast<uint32_t>(n);
     P.reconstruct = J.dest ? 1 : 0;
     P.compact = J.compact ? 1 : 0;
+    // passes == 1: every missing data row of every object is in this pass, so
+    // the kernel stores all k data slices unconditionally (DecodeMode kDecode)
+    P.mode = J.dest ? 1u : (passes == 1 ? 0u : 2u);
     hipError_t e = launch_decode(P, stream);
     if (e != hipSuccess) return e;
   }
