@@ -57,6 +57,7 @@ struct EncodeParams {
   uint32_t n_obj;
   uint32_t chunks, edge_chunks;  // set by the launcher (split_chunks)
   uint32_t xcd_split;            // set by the launcher (global_wave)
+  uint32_t run_chunks;           // set by the launcher (Sched)
 };
 
 // Per-object decode / reconstruct descriptor (device memory).
@@ -94,6 +95,7 @@ struct DecodeParams {
                             // 2 = generic (multi-pass decode)
   uint32_t chunks, edge_chunks;  // set by the launcher (split_chunks)
   uint32_t xcd_split;            // set by the launcher (global_wave)
+  uint32_t run_chunks;           // set by the launcher (Sched)
 };
 
 // Dispatch on (p.w, p.k) to the per-k instantiations (ec_dispatch.cpp).

@@ -340,13 +340,50 @@ __device__ __forceinline__ uint32_t global_wave(uint32_t xcd_split) {
   return b * kWavesPerBlock + wave_in_block();
 }
 
-struct Range {
-  uint32_t begin, end;
+// Chunk schedule of one wave over the flattened interior space [0, total).
+// run == 0: one contiguous range per wave.  run == R > 0: runs of R chunks
+// dealt round-robin to the waves (run r to wave r mod W), so at any moment
+// the waves of the grid work on one compact region of memory (DRAM row
+// locality) while each wave still walks R chunks in order.
+struct Sched {
+  uint32_t total, run, waves;
+  uint32_t begin, end;  // current run [begin, end)
+  __device__ __forceinline__ bool valid() const { return begin < end; }
+  // the run after the current one (begin >= end when there is none)
+  __device__ __forceinline__ void advance() {
+    if (run == 0) {
+      begin = end;
+      return;
+    }
+    const uint64_t nb = static_cast<uint64_t>(begin - begin % run) + static_cast<uint64_t>(waves) * run;
+    begin = nb < total ? static_cast<uint32_t>(nb) : total;
+    end = min(total, begin + run);
+  }
 };
-__device__ __forceinline__ Range wave_range(uint32_t total, uint32_t g) {
-  const uint64_t waves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
-  return {static_cast<uint32_t>(static_cast<uint64_t>(total) * g / waves),
-          static_cast<uint32_t>(static_cast<uint64_t>(total) * (g + 1) / waves)};
+__device__ __forceinline__ Sched make_sched(uint32_t total, uint32_t run, uint32_t g) {
+  const uint32_t waves = gridDim.x * kWavesPerBlock;
+  Sched S{total, run, waves, 0, 0};
+  if (run == 0) {
+    S.begin = static_cast<uint32_t>(static_cast<uint64_t>(total) * g / waves);
+    S.end = static_cast<uint32_t>(static_cast<uint64_t>(total) * (g + 1) / waves);
+  } else {
+    const uint64_t b = static_cast<uint64_t>(g) * run;
+    S.begin = b < total ? static_cast<uint32_t>(b) : total;
+    S.end = min(total, S.begin + run);
+  }
+  return S;
+}
+// Flattened index of the chunk after i in the wave's schedule (i itself when
+// i is the wave's last chunk); advances S across runs.
+__device__ __forceinline__ uint32_t sched_next(Sched& S, uint32_t i, bool& last) {
+  if (i + 1 < S.end) {
+    last = false;
+    return i + 1;
+  }
+  Sched n = S;
+  n.advance();
+  last = !n.valid();
+  return last ? i : n.begin;
 }
 
 __device__ __forceinline__ void next_chunk(uint32_t chunks, uint32_t& o, uint32_t& c) {
@@ -425,25 +462,24 @@ __global__ void __launch_bounds__(kThreadsPerBlock) encode_kernel(EncodeParams p
       if (p.data != nullptr) copy_headers(p.data + base, p.frag_stride, p.headers, K);
     }
   __syncthreads();
-  const Range r = wave_range(p.n_obj * p.chunks, g);
-  if (r.begin < r.end) {
+  Sched S = make_sched(p.n_obj * p.chunks, p.run_chunks, g);
+  if (S.valid()) {
     uint4 xa[K], xb[K];
-    uint32_t i = r.begin;
-    uint32_t o = i / p.chunks, c = i - o * p.chunks;
-    encode_load<K>(p, o, c, xa);
+    uint32_t i = S.begin;
+    encode_load<K>(p, i / p.chunks, i % p.chunks, xa);
     // two chunks per trip so cur / nxt stay compile-time register arrays
     while (true) {
-      uint32_t on = o, cn = c;
-      if (i + 1 < r.end) next_chunk(p.chunks, on, cn);
-      encode_item<F, K, NR>(p, o, c, on, cn, xa, xb);
-      if (++i >= r.end) break;
-      o = on;
-      c = cn;
-      if (i + 1 < r.end) next_chunk(p.chunks, on, cn);
-      encode_item<F, K, NR>(p, o, c, on, cn, xb, xa);
-      if (++i >= r.end) break;
-      o = on;
-      c = cn;
+      bool last;
+      uint32_t ni = sched_next(S, i, last);
+      encode_item<F, K, NR>(p, i / p.chunks, i % p.chunks, ni / p.chunks, ni % p.chunks, xa, xb);
+      if (last) break;
+      if (ni >= S.end) S.advance();
+      i = ni;
+      ni = sched_next(S, i, last);
+      encode_item<F, K, NR>(p, i / p.chunks, i % p.chunks, ni / p.chunks, ni % p.chunks, xb, xa);
+      if (last) break;
+      if (ni >= S.end) S.advance();
+      i = ni;
     }
   }
   const uint32_t n_edge = p.n_obj * p.edge_chunks;
@@ -803,12 +839,13 @@ decode_kernel(DecodeParams p) {
       copy_headers(p.out + static_cast<uint64_t>(o) * p.out_stride, 0,
                    p.headers + static_cast<uint64_t>(p.desc[o].header) * kHeaderBytes, 1);
   uint32_t cur_table = 0xFFFFFFFFu;
-  const Range r = wave_range(p.n_obj * p.chunks, g);
-  for (uint32_t i = r.begin; i < r.end;) {
-    const uint32_t o = i / p.chunks, c0 = i - o * p.chunks;
-    const uint32_t c1 = min(p.chunks, c0 + (r.end - i));
-    decode_run<F, K, MODE>(p, o, c0, c1, cur_table);
-    i += c1 - c0;
+  for (Sched S = make_sched(p.n_obj * p.chunks, p.run_chunks, g); S.valid(); S.advance()) {
+    for (uint32_t i = S.begin; i < S.end;) {  // split the run at object boundaries
+      const uint32_t o = i / p.chunks, c0 = i - o * p.chunks;
+      const uint32_t c1 = min(p.chunks, c0 + (S.end - i));
+      decode_run<F, K, MODE>(p, o, c0, c1, cur_table);
+      i += c1 - c0;
+    }
   }
   const uint32_t n_edge = p.n_obj * p.edge_chunks;
   for (uint32_t e = G - 1 - g; e < n_edge; e += G) decode_edge_item<F, K>(p, e, cur_table);
@@ -820,6 +857,16 @@ inline bool env_flag(const char* name, bool dflt) {
   const char* v = std::getenv(name);
   if (v == nullptr || *v == 0) return dflt;
   return v[0] != '0';
+}
+
+// Schedule tuning (read at each launch so tools/ab_bench.py can compare them
+// in one process): ECAMD_RUN = chunks per run (0 = one contiguous range per
+// wave).
+constexpr uint32_t kDefaultRunChunks = 8;
+inline uint32_t env_uint(const char* name, uint32_t dflt) {
+  const char* v = std::getenv(name);
+  if (v == nullptr || *v == 0) return dflt;
+  return static_cast<uint32_t>(std::strtoul(v, nullptr, 10));
 }
 
 // Resident workgroups for the kernel (a multiple of 8 when >= 8, so the XCD
@@ -880,6 +927,7 @@ hipError_t launch(Kern kern, Params p, size_t lds, uint32_t wave_items, hipStrea
   if (!lds_starts_at_zero(k)) return hipErrorInvalidKernelFile;
   const int grid = grid_for(k, lds, wave_items);
   p.xcd_split = (grid >= 8 && grid % 8 == 0 && env_flag("ECAMD_XCD", true)) ? 1u : 0u;
+  p.run_chunks = env_uint("ECAMD_RUN", kDefaultRunChunks);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreadsPerBlock), lds, stream, p);
   return hipGetLastError();
 }
