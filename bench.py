@@ -320,6 +320,17 @@ def host_resident(args, codec, host, stripes, masks, fs, bs, reps=3):
     B = host.shape[0]
     out = {}
     pinned = torch.from_numpy(host).pin_memory()
+    # the link itself: pinned H2D and D2H of the object batch (torch copies)
+    dev_buf = torch.empty(pinned.shape, dtype=torch.uint8, device=stripes.device)
+    for name, (dst, src) in (("h2d", (dev_buf, pinned)), ("d2h", (pinned, dev_buf))):
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        out[f"pcie_{name}_GiBps"] = round(pinned.numel() * reps / (time.perf_counter() - t0) / 2**30, 3)
+    del dev_buf
     hpar = torch.zeros((B, m, fs), dtype=torch.uint8).pin_memory()
     codec.encode_host(pinned, n, hpar)
     t0 = time.perf_counter()
@@ -344,6 +355,26 @@ def host_resident(args, codec, host, stripes, masks, fs, bs, reps=3):
         td = (time.perf_counter() - t0) / reps
         ok = ok and torch.equal(hout[:, :n], pinned[:, :n])
         out["host_resident_decode_GiBps"] = round(B * n / td / 2**30, 3)
+    # experiment: kernels streaming the pinned host arrays directly over PCIe
+    os.environ["ECAMD_HOST_DIRECT"] = "1"
+    try:
+        hpar2 = torch.zeros_like(hpar)
+        codec.encode_host(pinned, n, hpar2)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            codec.encode_host(pinned, n, hpar2)
+        out["host_direct_encode_GiBps"] = round(B * n / ((time.perf_counter() - t0) / reps) / 2**30, 3)
+        ok = ok and torch.equal(hpar2[:, :, :80 + bs], hpar[:, :, :80 + bs])
+        if args.second == "decode":
+            hout.zero_()
+            codec.decode_host(hfr, n, masks, hout)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                codec.decode_host(hfr, n, masks, hout)
+            out["host_direct_decode_GiBps"] = round(B * n / ((time.perf_counter() - t0) / reps) / 2**30, 3)
+            ok = ok and torch.equal(hout[:, :n], pinned[:, :n])
+    finally:
+        del os.environ["ECAMD_HOST_DIRECT"]
     out["host_resident_verified"] = bool(ok)
     out["host_resident_note"] = (f"pinned host in/out, {reps} reps of the batch; "
                                  "H2D/kernel/D2H pipelined on 3 streams")

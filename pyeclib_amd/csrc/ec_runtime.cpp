@@ -82,6 +82,11 @@ inline uint64_t get64(const void* p) {
   return v;
 }
 
+bool env_on(const char* name) {
+  const char* v = std::getenv(name);
+  return v != nullptr && v[0] != 0 && v[0] != '0';
+}
+
 bool write_legacy_crc() {
   const char* v = std::getenv("LIBERASURECODE_WRITE_LEGACY_CRC");
   if (!v) return false;
@@ -875,8 +880,34 @@ struct HostSide {
   uint64_t out_stride, out_last, out_skew;
 };
 
+// Pinned (page-locked, device-mapped) host memory covering [p, p + n)?
+bool device_mapped(const void* p, uint64_t n) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (a.type != hipMemoryTypeHost || a.devicePointer == nullptr) return false;
+  return a.devicePointer == p && n > 0;
+}
+
 template <class Run>
 int host_pipeline(Instance& I, int n_obj, const HostSide& H, Run run) {
+  // ECAMD_HOST_DIRECT=1 (experiment): when both host arrays are pinned and
+  // mapped, run the kernels on them directly -- every load and store crosses
+  // PCIe from the CUs, no staging copies -- in one launch on one stream.
+  const uint64_t in_total = static_cast<uint64_t>(n_obj - 1) * H.in_stride + H.in_last;
+  const uint64_t out_total = static_cast<uint64_t>(n_obj - 1) * H.out_stride + H.out_last;
+  if (env_on("ECAMD_HOST_DIRECT") && device_mapped(H.in, in_total) &&
+      device_mapped(H.out, out_total)) {
+    if (!I.hstream[0]) {
+      hipError_t e = hipStreamCreateWithFlags(&I.hstream[0], hipStreamNonBlocking);
+      if (e != hipSuccess) return hip_errno(e);
+    }
+    int rc = run(const_cast<uint8_t*>(H.in), H.out, 0, n_obj, I.hstream[0]);
+    const hipError_t e = hipStreamSynchronize(I.hstream[0]);
+    return rc < 0 ? rc : (e == hipSuccess ? 0 : hip_errno(e));
+  }
   // ~32 MiB of input per chunk, at least kHostStreams * 2 chunks when the
   // batch allows, so the three stages overlap for most of the batch
   int chunk = static_cast<int>(std::max<uint64_t>(1, (uint64_t(32) << 20) / H.in_stride));

@@ -200,3 +200,19 @@ def test_swift_mix_reduced_host_stream(gpu, oracle):
             out = torch.zeros((B, host.shape[1]), dtype=torch.uint8).pin_memory()
             codec.decode_host(hfr, n, masks, out)
             assert torch.equal(out[:, :n], pinned[:, :n]), (k, m, n)
+
+
+def test_swift_mix_tool_verifies(gpu):
+    """tools/swift_mix.py (configs[4] driver) on a reduced mix: its own
+    verification (parity vs the oracle, every decoded object) must pass."""
+    import json
+    import subprocess
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "swift_mix.py"),
+                        "--group-mib", "8", "--passes", "1", "--schemes", "6:2,12:4",
+                        "--sizes", "65536,1048576,16777216"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["verified"] is True
+    assert out["encode_GiBps"] > 0 and out["decode_GiBps"] > 0
+    assert len(out["groups"]) == 6

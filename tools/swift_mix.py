@@ -1,27 +1,39 @@
 #!/usr/bin/env python3
-"""BASELINE configs[4]: Swift-style mix, streaming encode from host memory.
+"""BASELINE configs[4]: Swift-style mix, streaming encode AND decode from host memory.
 
 Schemes k in {6, 10, 12} x m in {2, 4} (rs_vand, GF(2^16)), object sizes
 64 KiB, 256 KiB, 1 MiB, 4 MiB and 16 MiB.  Every (scheme, size) group holds
-about --group-mib of objects in pinned host memory; one pass encodes every
-group through ecamd_encode_host_batch (H2D, kernel and D2H pipelined over
-two streams; the data fragments are the host slices themselves, so only
-parity fragments come back), exactly the data flow of a Swift proxy that
-receives objects from a socket and writes fragments to disk.
+about --group-mib of objects in pinned host memory.  One pass:
+  * write path: every group through ecamd_encode_host_batch (H2D, kernel and
+    D2H pipelined over three streams; the data fragments are the host slices
+    themselves, so only parity fragments come back) -- a Swift proxy PUT:
+    object from a socket, fragments to the object servers;
+  * read path: every group through ecamd_decode_host_batch from the k
+    fragments a GET would fetch (m random fragments lost per object, the
+    first k survivors handed over, as pyeclib's decode uses them) -- a
+    Swift proxy GET.
+Rates are object bytes / wall time of the pass (host to host).
 
-One process per GPU (torchrun): every rank streams the whole mix (weak
-scaling, no collective on the data path).  Rank 0 prints one JSON line with
-the aggregate host-to-host GiB/s (object bytes), the per-group rates and,
-for contrast, the device-resident rate of the same groups.
+One process per GPU (every rank streams the whole mix; weak scaling, no
+collective on the data path).  `--gpus N` without a launcher starts
+torch.distributed.run itself as a child (as bench.py does).  Rank 0 prints
+one JSON line with the aggregate rates, per-group rates and, for contrast,
+the device-resident encode rate of the same groups.
 
-  python tools/swift_mix.py [--group-mib 64] [--passes 3]
-  torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/swift_mix.py
+Verification (every rank, outside the timed passes): in every group, the
+parity of up to --verify-objects objects is compared with the CPU oracle's
+(headers included), and EVERY decoded object with the original bytes; any
+mismatch exits non-zero.  "verified": true in the JSON line.
+
+  python tools/swift_mix.py [--group-mib 64] [--passes 3] [--gpus N]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import random
+import subprocess
 import sys
 import time
 
@@ -34,52 +46,157 @@ SCHEMES = [(6, 2), (6, 4), (10, 2), (10, 4), (12, 2), (12, 4)]
 SIZES = [64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20]
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--group-mib", type=int, default=64)
     ap.add_argument("--passes", type=int, default=3)
-    args = ap.parse_args()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--verify-objects", type=int, default=2,
+                    help="objects per group whose parity is checked against the oracle")
+    ap.add_argument("--schemes", default=None, help="e.g. 6:2,10:4 (default: all six)")
+    ap.add_argument("--sizes", default=None, help="e.g. 65536,1048576 (default: all five)")
+    return ap.parse_args(argv)
 
-    from pyeclib_amd import batch, shard
-    world, rank, local = shard.init("nccl")
-    import torch
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+
+def relaunch(args) -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+
+
+def build_groups(args, rank, batch, torch):
+    schemes = SCHEMES if not args.schemes else [
+        tuple(int(v) for v in s.split(":")) for s in args.schemes.split(",")]
+    sizes = SIZES if not args.sizes else [int(v) for v in args.sizes.split(",")]
     rng = np.random.Generator(np.random.PCG64(20261015 + rank))
-
+    pick = random.Random(77 + rank)
     groups = []
-    for k, m in SCHEMES:
+    for k, m in schemes:
         codec = batch.BatchCodec(k, m)
-        for size in SIZES:
+        for size in sizes:
             n = max(1, (args.group_mib << 20) // size)
             stride = (size + 255) // 256 * 256
             bs = batch.blocksize(k, size)
             fs = batch.frag_stride(bs)
             objs = torch.from_numpy(rng.integers(0, 256, (n, stride), dtype=np.uint8)).pin_memory()
             parity = torch.zeros((n, m, fs), dtype=torch.uint8).pin_memory()
+            masks = []
+            for _ in range(n):
+                lost = set(pick.sample(range(k + m), m))
+                masks.append(sum(1 << i for i in range(k + m) if i not in lost))
             groups.append({"k": k, "m": m, "size": size, "n": n, "codec": codec, "objs": objs,
-                           "parity": parity, "bs": bs})
+                           "parity": parity, "bs": bs, "fs": fs, "masks": masks,
+                           "frags": torch.zeros((n, k, fs), dtype=torch.uint8).pin_memory(),
+                           "out": torch.zeros((n, stride), dtype=torch.uint8).pin_memory()})
+    return groups
+
+
+def fill_read_fragments(g, torch):
+    """The k fragments each object's GET hands to decode (first k available,
+    ascending), from the host objects (data) and the encoded parity."""
+    k, bs, fl = g["k"], g["bs"], 80 + g["bs"]
+    from pyeclib_amd import _native  # noqa: F401 (library loaded)
+    objs = g["objs"].numpy()
+    par = g["parity"].numpy()
+    fr = g["frags"].numpy()
+    for o in range(g["n"]):
+        idx = [i for i in range(k + g["m"]) if g["masks"][o] >> i & 1][:k]
+        for c, i in enumerate(idx):
+            if i < k:
+                # data fragment = header (same fields as parity's, idx i) + padded slice
+                hdr = data_header(par[o, 0, :80], i)
+                fr[o, c, :80] = hdr
+                sl = objs[o, i * bs:min((i + 1) * bs, g["size"])]
+                fr[o, c, 80:80 + len(sl)] = sl
+                fr[o, c, 80 + len(sl):fl] = 0
+            else:
+                fr[o, c, :fl] = par[o, i - k, :fl]
+
+
+def data_header(parity0_hdr, idx):
+    """Header of data fragment idx, from parity fragment 0's header (the
+    fields differ only in idx and the metadata checksum)."""
+    import zlib
+    h = bytearray(parity0_hdr.tobytes())
+    h[0:4] = idx.to_bytes(4, "little")
+    h[67:71] = zlib.crc32(bytes(h[:59])).to_bytes(4, "little")
+    return np.frombuffer(bytes(h), dtype=np.uint8)
+
+
+def verify(groups, args):
+    from oracle import oracle as O
+    bad = []
+    for g in groups:
+        k, m, n, size, fl = g["k"], g["m"], g["n"], g["size"], 80 + g["bs"]
+        for o in range(min(n, args.verify_objects)):
+            want = O.encode(k, m, g["objs"][o, :size].numpy().tobytes())
+            for p in range(m):
+                if g["parity"][o, p, :fl].numpy().tobytes() != want[k + p]:
+                    bad.append((k, m, size, o, "parity", p))
+        if not np.array_equal(g["out"][:, :size].numpy(), g["objs"][:, :size].numpy()):
+            bad.append((k, m, size, "decode"))
+    return bad
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args))
+    import torch
+    from pyeclib_amd import batch, shard
+    world, rank, local = shard.rank_info()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    shard.init("nccl")
+
+    groups = build_groups(args, rank, batch, torch)
     total = sum(g["n"] * g["size"] for g in groups)
 
-    # warm-up (instance tables, staging buffers), then timed passes
+    # warm-up (instance tables, staging buffers), read-path inputs, then timed passes
     for g in groups:
         g["codec"].encode_host(g["objs"], g["size"], g["parity"])
+        fill_read_fragments(g, torch)
+        g["codec"].decode_host(g["frags"], g["size"], g["masks"], g["out"])
     shard.barrier()
     t0 = time.perf_counter()
     for _ in range(args.passes):
         for g in groups:
             t = time.perf_counter()
             g["codec"].encode_host(g["objs"], g["size"], g["parity"])
-            g.setdefault("t", []).append(time.perf_counter() - t)
+            g.setdefault("te", []).append(time.perf_counter() - t)
     shard.barrier()
-    elapsed = shard.max_over_ranks(time.perf_counter() - t0, device=dev) / args.passes
+    t_write = shard.max_over_ranks(time.perf_counter() - t0, device=dev) / args.passes
+    for g in groups:
+        g["out"].zero_()
+    shard.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.passes):
+        for g in groups:
+            t = time.perf_counter()
+            g["codec"].decode_host(g["frags"], g["size"], g["masks"], g["out"])
+            g.setdefault("td", []).append(time.perf_counter() - t)
+    shard.barrier()
+    t_read = shard.max_over_ranks(time.perf_counter() - t0, device=dev) / args.passes
+
+    bad = verify(groups, args)
+    ok = torch.tensor([0 if bad else 1], dtype=torch.int32, device=dev)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if bad:
+        print(f"rank {rank}: mismatches {bad[:5]}", file=sys.stderr, flush=True)
 
     # device-resident reference for the same groups
     t_dev = 0.0
     for g in groups:
         d_objs = g["objs"].to(dev)
-        d_par = torch.zeros((g["n"], g["m"], g["parity"].shape[2]), dtype=torch.uint8,
-                            device=dev)
+        d_par = torch.zeros((g["n"], g["m"], g["fs"]), dtype=torch.uint8, device=dev)
         g["codec"].encode(d_objs, g["size"], parity=d_par)
         torch.cuda.synchronize()
         t = time.perf_counter()
@@ -91,21 +208,29 @@ def main():
 
     if rank == 0:
         per_group = [{"k": g["k"], "m": g["m"], "object_bytes": g["size"], "objects": g["n"],
-                      "GiBps": round(g["n"] * g["size"] / min(g["t"]) / 2**30, 2)} for g in groups]
+                      "encode_GiBps": round(g["n"] * g["size"] / min(g["te"]) / 2**30, 2),
+                      "decode_GiBps": round(g["n"] * g["size"] / min(g["td"]) / 2**30, 2)}
+                     for g in groups]
         print(json.dumps({
-            "metric": "Swift-mix streaming encode GiB/s incl. pinned H2D/D2H (object bytes)",
-            "value": round(world * total / elapsed / 2**30, 3),
+            "metric": "Swift-mix streaming encode+decode GiB/s incl. pinned H2D/D2H (object bytes)",
+            "value": round(world * 2 * total / (t_write + t_read) / 2**30, 3),
             "unit": "GiB/s", "n_gpus": world, "passes": args.passes,
             "higher_is_better": True, "scaling": "weak",
-            "config": {"schemes": SCHEMES, "object_sizes": SIZES,
+            "encode_GiBps": round(world * total / t_write / 2**30, 3),
+            "decode_GiBps": round(world * total / t_read / 2**30, 3),
+            "verified": bool(ok.item()),
+            "config": {"schemes": sorted({(g["k"], g["m"]) for g in groups}),
+                       "object_sizes": sorted({g["size"] for g in groups}),
                        "group_bytes": args.group_mib << 20, "bytes_per_rank": total,
-                       "ec_type": "amd_rs_vand"},
-            "device_resident_GiBps_per_gpu": round(total / t_dev / 2**30, 3),
+                       "ec_type": "amd_rs_vand", "erasures_per_object_on_read": "m"},
+            "device_resident_encode_GiBps_per_gpu": round(total / t_dev / 2**30, 3),
             "groups": per_group,
         }), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    if not ok.item():
+        sys.exit(3)
 
 
 if __name__ == "__main__":
