@@ -55,9 +55,8 @@ struct EncodeParams {
   uint32_t row0, nrows;     // parity rows handled by this pass
   uint32_t bs;              // payload bytes per fragment
   uint32_t n_obj;
-  uint32_t chunks, edge_chunks;  // set by the launcher (split_chunks)
-  uint32_t xcd_split;            // set by the launcher (global_wave)
-  uint32_t run_chunks;           // set by the launcher (Sched)
+  uint32_t tiles, edge_tiles;  // set by the launcher: interior / edge items per object
+  uint32_t xcd_split;          // set by the launcher (item_range)
 };
 
 // Per-object decode / reconstruct descriptor (device memory).
@@ -93,9 +92,8 @@ struct DecodeParams {
   uint32_t mode;            // kernel variant (ec_kernels_impl.hpp DecodeMode): 0 = decode
                             // with every missing row in this pass, 1 = reconstruct,
                             // 2 = generic (multi-pass decode)
-  uint32_t chunks, edge_chunks;  // set by the launcher (split_chunks)
-  uint32_t xcd_split;            // set by the launcher (global_wave)
-  uint32_t run_chunks;           // set by the launcher (Sched)
+  uint32_t tiles, edge_tiles;  // set by the launcher: interior / edge items per object
+  uint32_t xcd_split;          // set by the launcher (item_range)
 };
 
 // Dispatch on (p.w, p.k) to the per-k instantiations (ec_dispatch.cpp).

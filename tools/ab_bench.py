@@ -3,7 +3,7 @@
 
 Each positional argument is one variant: "base" (no switches) or a
 comma-separated list of VAR=VAL environment settings, e.g.
-    python tools/ab_bench.py base ECAMD_RUN=0 ECAMD_RUN=4 ECAMD_XCD=0
+    python tools/ab_bench.py base ECAMD_DEC_OCC3=1 ECAMD_XCD=0
 The launcher reads the switches at every launch (ec_kernels_impl.hpp), so the
 variants run round-robin in one process on the same buffers (the workload of
 bench.py: k=10 m=4, 256 x 4 MiB, 4 erasures per object).  Every variant's
@@ -23,7 +23,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-KEYS = ["ECAMD_XCD", "ECAMD_RUN"]  # plus any other key a variant names
+KEYS = ["ECAMD_XCD", "ECAMD_DEC_OCC3"]  # plus any other key a variant names
 
 
 def parse_variant(text):

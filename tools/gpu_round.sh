@@ -26,7 +26,7 @@ for s in $STEPS; do
     (cd $R && timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1)
     tail -1 $O/smoke.log ;;
   ab)
-    (cd $R && timeout -k 10 400 python3 tools/ab_bench.py ${AB:-base ECAMD_RUN=0 ECAMD_RUN=1 ECAMD_RUN=2 ECAMD_RUN=4 ECAMD_RUN=16 ECAMD_RUN=32 ECAMD_XCD=0} > $O/ab.txt 2>&1)
+    (cd $R && timeout -k 10 400 python3 tools/ab_bench.py ${AB:-base ECAMD_DEC_OCC3=1 ECAMD_XCD=0} > $O/ab.txt 2>&1)
     cat $O/ab.txt ;;
   bench)
     (cd $R && timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err)
