@@ -38,6 +38,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstddef>
 #include <type_traits>
 #include <mutex>
 #include <unordered_map>
@@ -539,14 +540,14 @@ __device__ __forceinline__ void table_prefetch(const DecodeParams& p, uint32_t t
 }
 
 // Make d's table set current; returns its kb.  Block-uniform (barrier).
-template <class F, int K>
-__device__ __forceinline__ uint32_t ensure_tables(const DecodeParams& p, const ObjDesc& d,
-                                                  Slots& st, const TablePre<F, K>& pre) {
+template <class F, int K, class D>
+__device__ __forceinline__ uint32_t ensure_tables(const DecodeParams& p, const D& d, Slots& st,
+                                                  const TablePre<F, K>& pre) {
   constexpr uint32_t kSlot = table_slot_bytes(K, F::kW);
-  if (d.n_out != 0 && d.table != st.table) {
+  if (d.n_out() != 0 && d.table() != st.table) {
     st.slot ^= 1u;
     const uint32_t base = st.slot * kSlot;
-    if (pre.table == d.table) {
+    if (pre.table == d.table()) {
       auto* dst = lds_v4(base);
 #pragma unroll
       for (int i = 0; i < TablePre<F, K>::kPer; ++i) {
@@ -561,11 +562,11 @@ __device__ __forceinline__ uint32_t ensure_tables(const DecodeParams& p, const O
         }
       }
     } else {
-      load_tables(p.tables + static_cast<uint64_t>(d.table) * (K * F::kTableBytes / 4),
+      load_tables(p.tables + static_cast<uint64_t>(d.table()) * (K * F::kTableBytes / 4),
                   K * F::kTableBytes, base);
     }
     __syncthreads();
-    st.table = d.table;
+    st.table = d.table();
   }
   return F::kb(st.slot * kSlot);
 }
@@ -582,9 +583,43 @@ __host__ __device__ constexpr uint32_t chunk_stride() {
   return MODE == kReconstruct ? kChunkBytes : kChunkBytes - 16;
 }
 
+// An object's descriptor held in SGPRs.  The descriptor array is read with
+// vector loads (hipcc cannot prove the kernel's stores leave it untouched, so
+// it will not use scalar loads), and every field feeds a buffer soffset, a
+// uniform branch or the table switch: readfirstlane makes them provably
+// uniform -- without it hipcc wraps every buffer op in a waterfall loop
+// (measured: each load serialised behind s_waitcnt vmcnt(0);
+// cdna_hip_programming.md T20).
+// (Fields are extracted with shifts only: indexing w[] with a runtime value
+// would put the array in scratch memory and make the results non-uniform.)
+struct DescU {
+  uint32_t w[sizeof(ObjDesc) / 4];
+  // c: compile-time after unrolling
+  __device__ __forceinline__ uint32_t in_idx(int c) const {
+    return (w[c >> 2] >> (8 * (c & 3))) & 0xFFu;
+  }
+  // q: runtime (0..3)
+  __device__ __forceinline__ uint32_t out_idx(uint32_t q) const { return (w[8] >> (8 * q)) & 0xFFu; }
+  __device__ __forceinline__ uint32_t n_out() const { return w[9] & 0xFFu; }
+  __device__ __forceinline__ uint32_t copy_inputs() const { return (w[9] >> 8) & 0xFFu; }
+  __device__ __forceinline__ uint32_t table() const { return w[10]; }
+  __device__ __forceinline__ uint32_t header() const { return w[11]; }
+};
+static_assert(offsetof(ObjDesc, out_idx) == 32 && offsetof(ObjDesc, n_out) == 36 &&
+                  offsetof(ObjDesc, copy_inputs) == 37 && offsetof(ObjDesc, table) == 40 &&
+                  offsetof(ObjDesc, header) == 44 && sizeof(ObjDesc) % 4 == 0,
+              "DescU mirrors ObjDesc");
+__device__ __forceinline__ DescU load_desc(const DecodeParams& p, uint32_t o) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(p.desc + o);
+  DescU u;
+#pragma unroll
+  for (uint32_t i = 0; i < sizeof(ObjDesc) / 4; ++i) u.w[i] = __builtin_amdgcn_readfirstlane(src[i]);
+  return u;
+}
+
 // Fragment group position of input c.
-__device__ __forceinline__ uint32_t in_pos(const DecodeParams& p, const ObjDesc& d, int c) {
-  return p.compact ? static_cast<uint32_t>(c) : d.in_idx[c];
+__device__ __forceinline__ uint32_t in_pos(const DecodeParams& p, const DescU& d, int c) {
+  return p.compact ? static_cast<uint32_t>(c) : d.in_idx(c);
 }
 
 template <int MODE>
@@ -596,9 +631,8 @@ __device__ __forceinline__ void dec_item_pos(const DecodeParams& p, uint32_t w, 
 }
 
 template <int K>
-__device__ __forceinline__ void decode_load(const DecodeParams& p, uint32_t o, uint32_t x,
-                                            uint4 (&v)[K]) {
-  const ObjDesc& d = p.desc[o];
+__device__ __forceinline__ void decode_load(const DecodeParams& p, uint32_t o, const DescU& d,
+                                            uint32_t x, uint4 (&v)[K]) {
   const Rsrc in = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride);
 #pragma unroll
   for (int j = 0; j < K; ++j)
@@ -668,8 +702,8 @@ __device__ __forceinline__ void st_unit(Rsrc out, uint32_t vst, uint32_t soff, c
 // as many as there are missing data slices, e -- are the last e.  After the
 // products, row q overwrites parity input K-e+q: cur[c] then holds data slice
 // slice_of(c) for every c, and all K slices are stored unconditionally.
-__device__ __forceinline__ uint32_t slice_of(const ObjDesc& d, uint32_t e, int K, int c) {
-  return c < K - static_cast<int>(e) ? d.in_idx[c] : d.out_idx[c - (K - static_cast<int>(e))];
+__device__ __forceinline__ uint32_t slice_of(const DescU& d, uint32_t e, int K, int c) {
+  return c < K - static_cast<int>(e) ? d.in_idx(c) : d.out_idx(c - (K - static_cast<int>(e)));
 }
 
 template <class F, int K>
@@ -698,15 +732,13 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
   uint32_t o, x, on, xn;
   dec_item_pos<MODE>(p, w, o, x);
   dec_item_pos<MODE>(p, wn, on, xn);
-  decode_load<K>(p, on, xn, nxt);
-  const ObjDesc& d = p.desc[o];
+  const DescU dn = load_desc(p, on);
+  decode_load<K>(p, on, dn, xn, nxt);
+  const DescU d = load_desc(p, o);
   const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
-  {
-    const ObjDesc& dn = p.desc[on];
-    if (dn.n_out != 0 && dn.table != st.table && dn.table != pre.table)
-      table_prefetch<F, K>(p, dn.table, pre);
-  }
-  const uint32_t n_out = d.n_out;
+  if (dn.n_out() != 0 && dn.table() != st.table && dn.table() != pre.table)
+    table_prefetch<F, K>(p, dn.table(), pre);
+  const uint32_t n_out = d.n_out();
   typename F::Acc s;
   F::zero(s);
   if (n_out != 0) {
@@ -728,10 +760,10 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
         st_unit(out, vst, off + x, cur[j], off & 15u);
       }
     } else {
-      if (d.copy_inputs) {
+      if (d.copy_inputs()) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-          const uint32_t idx = d.in_idx[j];
+          const uint32_t idx = d.in_idx(j);
           if (idx < static_cast<uint32_t>(K)) {
             const uint32_t off = idx * p.bs;
             st_unit(out, vst, off + x, cur[j], off & 15u);
@@ -741,7 +773,7 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
 #pragma unroll
       for (int q = 0; q < kRowsPerPass; ++q) {
         if (q < static_cast<int>(n_out)) {
-          const uint32_t off = d.out_idx[q] * p.bs;
+          const uint32_t off = d.out_idx(q) * p.bs;
           st_unit(out, vst, off + x, F::row(s, q), off & 15u);
         }
       }
@@ -761,7 +793,7 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
   const uint32_t tail0 = p.tiles * kWavesPerBlock * chunk_stride<MODE>();
   const bool head = MODE != kReconstruct && ei == 0;
   const uint32_t q0 = head ? 0u : tail0 + (ei - (MODE != kReconstruct ? 1u : 0u)) * 4096u;
-  const ObjDesc& d = p.desc[o];
+  const DescU d = load_desc(p, o);
   const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
   const uint32_t t = q0 + threadIdx.x * 16;
   if (t >= p.bs) return;
@@ -774,13 +806,13 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
     x[j] = *reinterpret_cast<const uint4*>(in + in_pos(p, d, j) * p.frag_stride);
   typename F::Acc s;
   F::zero(s);
-  if (d.n_out != 0) {
+  if (d.n_out() != 0) {
 #pragma unroll
     for (int j = 0; j < K; ++j) F::mac(kb, j * F::kTableBytes, x[j], s);
   }
   F::pin(s);
   if (MODE == kReconstruct) {
-    if (d.n_out != 0) store_window(out + kHeaderBytes, t, F::row(s, 0), tail0, p.bs);
+    if (d.n_out() != 0) store_window(out + kHeaderBytes, t, F::row(s, 0), tail0, p.bs);
     return;
   }
   // window of slice j: [lo_j, hi_j) in slice positions
@@ -791,18 +823,18 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
     hi = head ? 16 - sh : valid;
     if (hi > valid) hi = valid;
   };
-  if (d.copy_inputs) {
+  if (d.copy_inputs()) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      const uint32_t idx = d.in_idx[j];
+      const uint32_t idx = d.in_idx(j);
       if (idx >= K) continue;
       int64_t lo, hi;
       window(idx, lo, hi);
       store_window(out + static_cast<uint64_t>(idx) * p.bs, t, x[j], lo, hi);
     }
   }
-  for (uint32_t q = 0; q < d.n_out; ++q) {
-    const uint32_t idx = d.out_idx[q];
+  for (uint32_t q = 0; q < d.n_out(); ++q) {
+    const uint32_t idx = d.out_idx(q);
     int64_t lo, hi;
     window(idx, lo, hi);
     store_window(out + static_cast<uint64_t>(idx) * p.bs, t, F::row(s, q), lo, hi);
@@ -818,7 +850,7 @@ decode_kernel(DecodeParams p) {
   if (MODE == kReconstruct && p.headers != nullptr)
     for (uint32_t o = blockIdx.x; o < p.n_obj; o += gridDim.x)
       block_headers(p.out + static_cast<uint64_t>(o) * p.out_stride, 0,
-                    p.headers + static_cast<uint64_t>(p.desc[o].header) * kHeaderBytes, 1);
+                    p.headers + static_cast<uint64_t>(load_desc(p, o).header()) * kHeaderBytes, 1);
   Slots st{0xFFFFFFFFu, 1u};
   TablePre<F, K> pre;
   pre.table = 0xFFFFFFFFu;
@@ -832,11 +864,9 @@ decode_kernel(DecodeParams p) {
     uint4 xa[K], xb[K];
     uint32_t o, x;
     dec_item_pos<MODE>(p, w, o, x);
-    decode_load<K>(p, o, x, xa);
-    {
-      const ObjDesc& d0 = p.desc[o];
-      if (d0.n_out != 0 && d0.table != st.table) table_prefetch<F, K>(p, d0.table, pre);
-    }
+    const DescU d0 = load_desc(p, o);
+    decode_load<K>(p, o, d0, x, xa);
+    if (d0.n_out() != 0 && d0.table() != st.table) table_prefetch<F, K>(p, d0.table(), pre);
     while (true) {
       uint32_t wn = w + r.step < r.end ? w + r.step : w;
       decode_item<F, K, MODE>(p, w, wn, st, pre, xa, xb);
