@@ -42,12 +42,15 @@ for s in $STEPS; do
     (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run \
       -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host > $O/pmc_write.log 2>&1)
     python3 $R/tools/pmc_summary.py $O/pmc_fetch $O/pmc_write $O/pmc_summary.json ;;
+  list)
+    (cd /tmp && timeout -k 10 120 rocprofv3 -L > $O/counters.txt 2>&1) || true
+    grep -c . $O/counters.txt ;;
   sq)
-    for f in pmc1 pmc2; do
+    for f in pmc1 pmc2 pmc3; do
       (cd /tmp && timeout -s KILL 150 rocprofv3 -i $R/tools/$f.txt --output-format csv -d $O/sq_$f -o run \
         -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host > $O/sq_$f.log 2>&1)
     done
-    python3 $R/tools/pmc_table.py $O/sq_pmc1 $O/sq_pmc2 > $O/sq_table.txt 2>&1 || true
+    python3 $R/tools/pmc_table.py $O/sq_pmc1 $O/sq_pmc2 $O/sq_pmc3 > $O/sq_table.txt 2>&1 || true
     cat $O/sq_table.txt ;;
   *) echo "unknown step $s"; exit 2 ;;
   esac
