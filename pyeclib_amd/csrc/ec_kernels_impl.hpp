@@ -93,24 +93,35 @@ __device__ __forceinline__ void st_stream(void* p, const uint4& x) {
 // 64-bit address pair each.  aux 2 = nt (streamed once).
 typedef __amdgpu_buffer_rsrc_t Rsrc;
 constexpr int kNt = 2;
-__device__ __forceinline__ Rsrc rsrc(const void* base) {
+// `records` = bytes addressable through the descriptor; a zero-record
+// descriptor turns its loads into zeros with no memory access at all (the
+// range check drops them), which is how a wave's last item "prefetches"
+// nothing while keeping the instruction stream -- and so hipcc's wait
+// counts -- identical to every other item.
+__device__ __forceinline__ Rsrc rsrc(const void* base, int records = -1) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
   return __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, -1, 0x00020000);
+      reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, records, 0x00020000);
 }
+// Cache policy of the interior streams (compile time; POL bits):
+// nontemporal by default, kPolLoadsCached / kPolStoresCached switch loads /
+// stores to the default policy (A/B variants of the benchmark case).
+constexpr int kPolLoadsCached = 1, kPolStoresCached = 2;
+template <bool CACHED = false>
 __device__ __forceinline__ uint4 buf_ld(Rsrc r, uint32_t voff, uint32_t soff) {
-  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, kNt);
+  const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, CACHED ? 0 : kNt);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+template <bool CACHED = false>
 __device__ __forceinline__ void buf_st(Rsrc r, uint32_t voff, uint32_t soff, const uint4& x) {
   v4u v;
   v.x = x.x;
   v.y = x.y;
   v.z = x.z;
   v.w = x.w;
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, kNt);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, CACHED ? 0 : kNt);
 }
 
 // a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
@@ -374,28 +385,30 @@ __device__ __forceinline__ void enc_item_pos(const EncodeParams& p, uint32_t w, 
   x = (w - o * p.tiles) * (kWavesPerBlock * kChunkBytes) + wave_in_block() * kChunkBytes;
 }
 
-template <int K>
+template <int K, int POL>
 __device__ __forceinline__ void encode_load(const EncodeParams& p, uint32_t o, uint32_t x,
-                                            uint4 (&v)[K]) {
-  const Rsrc r = rsrc(p.objs + static_cast<uint64_t>(o) * p.obj_stride);
+                                            uint4 (&v)[K], bool none = false) {
+  const Rsrc r = rsrc(p.objs + static_cast<uint64_t>(o) * p.obj_stride, none ? 0 : -1);
 #pragma unroll
-  for (int j = 0; j < K; ++j) v[j] = buf_ld(r, lane_id() * 16, j * p.bs + x);
+  for (int j = 0; j < K; ++j)
+    v[j] = buf_ld<(POL & kPolLoadsCached) != 0>(r, lane_id() * 16, j * p.bs + x);
 }
 
 // One interior item with its inputs in `cur`; first issues the loads of the
 // block's next item into `nxt` so they are in flight while this item's table
-// lookups run (the last item re-loads itself: an L2 hit).  Every memory
+// lookups run (the last item's "next" loads go through a zero-record
+// descriptor: no memory traffic).  Every memory
 // operation in the loop body is unconditional, so hipcc's s_waitcnt before
 // cur[j] waits only for cur's own loads (a branch around a load or store
 // makes it fall back to the shortest path's count -- measured in round 1 as
 // waiting for the prefetch too, which serialised memory and compute).
-template <class F, int K, int NR>
+template <class F, int K, int NR, int POL>
 __device__ __forceinline__ void encode_item(const EncodeParams& p, uint32_t w, uint32_t wn,
                                             uint4 (&cur)[K], uint4 (&nxt)[K]) {
   uint32_t o, x, on, xn;
   enc_item_pos(p, w, o, x);
   enc_item_pos(p, wn, on, xn);
-  encode_load<K>(p, on, xn, nxt);
+  encode_load<K, POL>(p, on, xn, nxt, wn == w);
   typename F::Acc s;
   F::zero(s);
 #pragma unroll
@@ -404,7 +417,8 @@ __device__ __forceinline__ void encode_item(const EncodeParams& p, uint32_t w, u
   const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
   const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x;
 #pragma unroll
-  for (int q = 0; q < NR; ++q) buf_st(par, lane_id() * 16, soff + q * p.frag_stride, F::row(s, q));
+  for (int q = 0; q < NR; ++q)
+    buf_st<(POL & kPolStoresCached) != 0>(par, lane_id() * 16, soff + q * p.frag_stride, F::row(s, q));
 }
 
 // Edge item: payload tail and chunks reaching the zero padding past obj_len
@@ -431,7 +445,7 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
   for (int q = 0; q < NR; ++q) store_partial(par + q * p.frag_stride, F::row(s, q), rem);
 }
 
-template <class F, int K, int NR>
+template <class F, int K, int NR, int POL>
 __global__ void __launch_bounds__(kThreadsPerBlock) encode_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
   if (p.headers != nullptr && p.row0 == 0)
@@ -452,15 +466,15 @@ __global__ void __launch_bounds__(kThreadsPerBlock) encode_kernel(EncodeParams p
     uint4 xa[K], xb[K];
     uint32_t o, x;
     enc_item_pos(p, w, o, x);
-    encode_load<K>(p, o, x, xa);
+    encode_load<K, POL>(p, o, x, xa);
     // two items per trip so cur / nxt stay compile-time register arrays
     while (true) {
       uint32_t wn = w + r.step < r.end ? w + r.step : w;
-      encode_item<F, K, NR>(p, w, wn, xa, xb);
+      encode_item<F, K, NR, POL>(p, w, wn, xa, xb);
       if (wn == w) break;
       w = wn;
       wn = w + r.step < r.end ? w + r.step : w;
-      encode_item<F, K, NR>(p, w, wn, xb, xa);
+      encode_item<F, K, NR, POL>(p, w, wn, xb, xa);
       if (wn == w) break;
       w = wn;
     }
@@ -577,10 +591,15 @@ enum DecodeMode : int {
   kDecodeGeneric = 2  // more than 4 missing data fragments (several passes)
 };
 
-// Chunk stride of a mode: decode overlaps one lane (realigned slices).
-template <int MODE>
+// Chunk stride: decode overlaps one lane (realigned slices) unless PLAIN
+// (lane stores at their natural, unaligned positions -- kept for A/B).
+template <int MODE, bool PLAIN>
+__host__ __device__ constexpr bool overlaps() {
+  return MODE != kReconstruct && !PLAIN;
+}
+template <int MODE, bool PLAIN>
 __host__ __device__ constexpr uint32_t chunk_stride() {
-  return MODE == kReconstruct ? kChunkBytes : kChunkBytes - 16;
+  return overlaps<MODE, PLAIN>() ? kChunkBytes - 16 : kChunkBytes;
 }
 
 // An object's descriptor held in SGPRs.  The descriptor array is read with
@@ -622,21 +641,22 @@ __device__ __forceinline__ uint32_t in_pos(const DecodeParams& p, const DescU& d
   return p.compact ? static_cast<uint32_t>(c) : d.in_idx(c);
 }
 
-template <int MODE>
+template <int MODE, bool PLAIN>
 __device__ __forceinline__ void dec_item_pos(const DecodeParams& p, uint32_t w, uint32_t& o,
                                              uint32_t& x) {
+  constexpr uint32_t kStride = chunk_stride<MODE, PLAIN>();
   o = w / p.tiles;
-  x = (w - o * p.tiles) * (kWavesPerBlock * chunk_stride<MODE>()) +
-      wave_in_block() * chunk_stride<MODE>();
+  x = (w - o * p.tiles) * (kWavesPerBlock * kStride) + wave_in_block() * kStride;
 }
 
-template <int K>
+template <int K, int POL>
 __device__ __forceinline__ void decode_load(const DecodeParams& p, uint32_t o, const DescU& d,
-                                            uint32_t x, uint4 (&v)[K]) {
-  const Rsrc in = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride);
+                                            uint32_t x, uint4 (&v)[K], bool none = false) {
+  const Rsrc in = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride, none ? 0 : -1);
 #pragma unroll
   for (int j = 0; j < K; ++j)
-    v[j] = buf_ld(in, lane_id() * 16, in_pos(p, d, j) * p.frag_stride + kHeaderBytes + x);
+    v[j] = buf_ld<(POL & kPolLoadsCached) != 0>(
+        in, lane_id() * 16, in_pos(p, d, j) * p.frag_stride + kHeaderBytes + x);
 }
 
 // Output descriptor: 2 GiB - 1 records, so a voffset of kDrop (2 GiB) makes
@@ -660,10 +680,11 @@ __device__ __forceinline__ uint32_t shr1(uint32_t v) {
 // aligned unit at soff + 16*L - s, lane 0 is dropped (vst = kDrop).  Only
 // the dwords of lane L-1 that the unit uses are moved (d = (16 - s) / 4).
 // Every path issues exactly one store instruction.
+template <bool CACHED>
 __device__ __forceinline__ void st_unit(Rsrc out, uint32_t vst, uint32_t soff, const uint4& v,
                                         uint32_t s) {
   if (s == 0) {
-    buf_st(out, vst, soff, v);
+    buf_st<CACHED>(out, vst, soff, v);
     return;
   }
   const uint32_t r = (16u - s) & 3u;
@@ -694,7 +715,7 @@ __device__ __forceinline__ void st_unit(Rsrc out, uint32_t vst, uint32_t soff, c
       break;
     }
   }
-  buf_st(out, vst, soff - s, u);
+  buf_st<CACHED>(out, vst, soff - s, u);
 }
 
 // kDecode: the k inputs are the first k available fragments in ascending
@@ -725,15 +746,15 @@ __device__ __forceinline__ void place_rows(const typename F::Acc& s, uint32_t e,
 
 // One interior decode / reconstruct item with inputs in `cur`; prefetches the
 // block's next item (payloads into `nxt`, its table set into `pre`).
-template <class F, int K, int MODE>
+template <class F, int K, int MODE, bool PLAIN, int POL>
 __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, uint32_t wn,
                                             Slots& st, TablePre<F, K>& pre, uint4 (&cur)[K],
                                             uint4 (&nxt)[K]) {
   uint32_t o, x, on, xn;
-  dec_item_pos<MODE>(p, w, o, x);
-  dec_item_pos<MODE>(p, wn, on, xn);
+  dec_item_pos<MODE, PLAIN>(p, w, o, x);
+  dec_item_pos<MODE, PLAIN>(p, wn, on, xn);
   const DescU dn = load_desc(p, on);
-  decode_load<K>(p, on, dn, xn, nxt);
+  decode_load<K, POL>(p, on, dn, xn, nxt, wn == w);
   const DescU d = load_desc(p, o);
   const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
   if (dn.n_out() != 0 && dn.table() != st.table && dn.table() != pre.table)
@@ -746,37 +767,36 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
     for (int j = 0; j < K; ++j) F::mac(kb, j * F::kTableBytes, cur[j], s);
   }
   F::pin(s);
+  constexpr bool kStC = (POL & kPolStoresCached) != 0;
   uint8_t* const outp = p.out + static_cast<uint64_t>(o) * p.out_stride;
   if constexpr (MODE == kReconstruct) {
-    buf_st(rsrc(outp), lane_id() * 16, kHeaderBytes + x, F::row(s, 0));
+    buf_st<kStC>(rsrc(outp), lane_id() * 16, kHeaderBytes + x, F::row(s, 0));
   } else {
-    const Rsrc out = rsrc_out(outp);
-    const uint32_t vst = lane_id() == 0 ? kDrop : lane_id() * 16;
+    // overlap: lane 0 only carries the previous chunk's bytes, its store is
+    // dropped; plain: every lane stores its own 16 B where they belong
+    const Rsrc out = PLAIN ? rsrc(outp) : rsrc_out(outp);
+    const uint32_t vst = (!PLAIN && lane_id() == 0) ? kDrop : lane_id() * 16;
+    auto put = [&](uint32_t off, const uint4& v) {
+      if constexpr (PLAIN)
+        buf_st<kStC>(out, vst, off + x, v);
+      else
+        st_unit<kStC>(out, vst, off + x, v, off & 15u);
+    };
     if constexpr (MODE == kDecode) {
       place_rows<F, K>(s, n_out, cur);
 #pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const uint32_t off = slice_of(d, n_out, K, j) * p.bs;
-        st_unit(out, vst, off + x, cur[j], off & 15u);
-      }
+      for (int j = 0; j < K; ++j) put(slice_of(d, n_out, K, j) * p.bs, cur[j]);
     } else {
       if (d.copy_inputs()) {
 #pragma unroll
         for (int j = 0; j < K; ++j) {
           const uint32_t idx = d.in_idx(j);
-          if (idx < static_cast<uint32_t>(K)) {
-            const uint32_t off = idx * p.bs;
-            st_unit(out, vst, off + x, cur[j], off & 15u);
-          }
+          if (idx < static_cast<uint32_t>(K)) put(idx * p.bs, cur[j]);
         }
       }
 #pragma unroll
-      for (int q = 0; q < kRowsPerPass; ++q) {
-        if (q < static_cast<int>(n_out)) {
-          const uint32_t off = d.out_idx(q) * p.bs;
-          st_unit(out, vst, off + x, F::row(s, q), off & 15u);
-        }
-      }
+      for (int q = 0; q < kRowsPerPass; ++q)
+        if (q < static_cast<int>(n_out)) put(d.out_idx(q) * p.bs, F::row(s, q));
     }
   }
 }
@@ -785,14 +805,15 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
 // clipped to each output's window.  Decode: head item (window [0, 16 - s))
 // and tail items (window [tiles*4032 + 16 - s, object bytes of the slice)).
 // Reconstruct: tail items [tiles*4096, bs).
-template <class F, int K, int MODE>
+template <class F, int K, int MODE, bool PLAIN>
 __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t e, Slots& st,
                                                  const TablePre<F, K>& pre) {
+  constexpr bool kOv = overlaps<MODE, PLAIN>();
   const uint32_t o = e / p.edge_tiles;
   const uint32_t ei = e - o * p.edge_tiles;
-  const uint32_t tail0 = p.tiles * kWavesPerBlock * chunk_stride<MODE>();
-  const bool head = MODE != kReconstruct && ei == 0;
-  const uint32_t q0 = head ? 0u : tail0 + (ei - (MODE != kReconstruct ? 1u : 0u)) * 4096u;
+  const uint32_t tail0 = p.tiles * kWavesPerBlock * chunk_stride<MODE, PLAIN>();
+  const bool head = kOv && ei == 0;
+  const uint32_t q0 = head ? 0u : tail0 + (ei - (kOv ? 1u : 0u)) * 4096u;
   const DescU d = load_desc(p, o);
   const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
   const uint32_t t = q0 + threadIdx.x * 16;
@@ -819,7 +840,7 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
   auto window = [&](uint32_t j, int64_t& lo, int64_t& hi) {
     const uint32_t sh = (j * p.bs) & 15u;
     const int64_t valid = object_bytes(j, p.bs, 0, p.obj_len);
-    lo = head ? 0 : static_cast<int64_t>(tail0) + 16 - sh;
+    lo = head ? 0 : static_cast<int64_t>(tail0) + (kOv ? 16 - sh : 0);
     hi = head ? 16 - sh : valid;
     if (hi > valid) hi = valid;
   };
@@ -844,7 +865,7 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
 // OCC = minimum waves per SIMD the register allocation must allow (hipcc
 // left alone spends ~140 VGPRs on the decode variants: 3 waves per SIMD; 4
 // fits in 128 VGPRs with a few spills around the table prefetch).
-template <class F, int K, int MODE, int OCC>
+template <class F, int K, int MODE, int OCC, bool PLAIN, int POL>
 __global__ void __launch_bounds__(kThreadsPerBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8)))
 decode_kernel(DecodeParams p) {
   if (MODE == kReconstruct && p.headers != nullptr)
@@ -857,23 +878,23 @@ decode_kernel(DecodeParams p) {
   // edge items first, on the highest-numbered blocks
   const uint32_t n_edge = p.n_obj * p.edge_tiles;
   for (uint32_t e = gridDim.x - 1 - blockIdx.x; e < n_edge; e += gridDim.x)
-    decode_edge_item<F, K, MODE>(p, e, st, pre);
+    decode_edge_item<F, K, MODE, PLAIN>(p, e, st, pre);
   const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
   uint32_t w = r.begin;
   if (w < r.end) {
     uint4 xa[K], xb[K];
     uint32_t o, x;
-    dec_item_pos<MODE>(p, w, o, x);
+    dec_item_pos<MODE, PLAIN>(p, w, o, x);
     const DescU d0 = load_desc(p, o);
-    decode_load<K>(p, o, d0, x, xa);
+    decode_load<K, POL>(p, o, d0, x, xa);
     if (d0.n_out() != 0 && d0.table() != st.table) table_prefetch<F, K>(p, d0.table(), pre);
     while (true) {
       uint32_t wn = w + r.step < r.end ? w + r.step : w;
-      decode_item<F, K, MODE>(p, w, wn, st, pre, xa, xb);
+      decode_item<F, K, MODE, PLAIN, POL>(p, w, wn, st, pre, xa, xb);
       if (wn == w) break;
       w = wn;
       wn = w + r.step < r.end ? w + r.step : w;
-      decode_item<F, K, MODE>(p, w, wn, st, pre, xb, xa);
+      decode_item<F, K, MODE, PLAIN, POL>(p, w, wn, st, pre, xb, xa);
       if (wn == w) break;
       w = wn;
     }
@@ -928,6 +949,7 @@ hipError_t launch(Kern kern, Params p, size_t lds, uint32_t items, hipStream_t s
   if (!lds_starts_at_zero(k)) return hipErrorInvalidKernelFile;
   const int grid = grid_for(k, lds, items);
   p.xcd_split = (grid >= 8 && grid % 8 == 0 && env_flag("ECAMD_XCD", true)) ? 1u : 0u;
+
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreadsPerBlock), lds, stream, p);
   return hipGetLastError();
 }
@@ -940,6 +962,13 @@ inline int64_t last_room(uint32_t bs, uint64_t obj_len, uint32_t k) {
   return room < 0 ? 0 : room;
 }
 
+// Cache-policy variant requested through the environment (A/B of the
+// benchmark case only): ECAMD_LD_CACHED=1 / ECAMD_ST_CACHED=1.
+inline int env_policy() {
+  return (env_flag("ECAMD_LD_CACHED", false) ? kPolLoadsCached : 0) |
+         (env_flag("ECAMD_ST_CACHED", false) ? kPolStoresCached : 0);
+}
+
 template <class F, int K, int NR>
 hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   // interior tiles: 4 KiB of positions ending at or before min(bs, room)
@@ -948,7 +977,16 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   p.edge_tiles = (p.bs + tile - 1) / tile - p.tiles;
   const uint32_t items = std::max(std::max(p.n_obj * p.tiles, p.n_obj * p.edge_tiles),
                                   p.headers ? p.n_obj : 0u);
-  hipError_t e = launch(encode_kernel<F, K, NR>, p, K * F::kTableBytes, items, stream);
+  hipError_t e;
+  const int pol = (K == 10 && NR == 4) ? env_policy() : 0;
+  if (pol == 0)
+    e = launch(encode_kernel<F, K, NR, 0>, p, K * F::kTableBytes, items, stream);
+  else if constexpr (K == 10 && NR == 4)
+    e = pol == 1   ? launch(encode_kernel<F, K, NR, 1>, p, K * F::kTableBytes, items, stream)
+        : pol == 2 ? launch(encode_kernel<F, K, NR, 2>, p, K * F::kTableBytes, items, stream)
+                   : launch(encode_kernel<F, K, NR, 3>, p, K * F::kTableBytes, items, stream);
+  else
+    e = hipErrorInvalidValue;
   if (e != hipSuccess || p.data == nullptr || p.row0 != 0) return e;
   return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + tile - 1) / tile), stream);
 }
@@ -971,32 +1009,53 @@ hipError_t launch_encode_rows(const EncodeParams& p, hipStream_t stream) {
 
 constexpr int kDecodeOcc = 4;
 
-template <class F, int K, int MODE>
-hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
-  if (MODE == kReconstruct) {
-    // whole payload, 4 KiB tiles, tail items
-    const uint32_t tile = kWavesPerBlock * kChunkBytes;
-    p.tiles = p.bs / tile;
+template <class F, int K, int MODE, int OCC, bool PLAIN, int POL = 0>
+hipError_t launch_decode_variant(DecodeParams p, hipStream_t stream) {
+  constexpr uint32_t tile = kWavesPerBlock * chunk_stride<MODE, PLAIN>();
+  if constexpr (!overlaps<MODE, PLAIN>()) {
+    // 4 KiB tiles over the payload (reconstruct) or up to the object's end
+    const int64_t lim = MODE == kReconstruct ? static_cast<int64_t>(p.bs)
+                                             : last_room(p.bs, p.obj_len, K);
+    p.tiles = static_cast<uint32_t>(lim / tile);
     p.edge_tiles = (p.bs + tile - 1) / tile - p.tiles;
   } else {
-    // interior: tile T covers loads [T*4032, T*4032 + 4048) and slice bytes
-    // up to T*4032 + 4048 - s; it must stay inside min(bs, room)
-    const uint32_t tile = kWavesPerBlock * chunk_stride<MODE>();
+    // tile T covers loads [T*4032, T*4032 + 4048) and slice bytes up to
+    // T*4032 + 4048 - s; it must stay inside min(bs, room)
     const int64_t lim = last_room(p.bs, p.obj_len, K);
     p.tiles = lim >= tile + 16 ? static_cast<uint32_t>((lim - 16) / tile) : 0u;
-    const uint32_t tail0 = p.tiles * tile;
-    p.edge_tiles = 1 + (p.bs - tail0 + 4095) / 4096;  // head + tail items
+    p.edge_tiles = 1 + (p.bs - p.tiles * tile + 4095) / 4096;  // head + tail items
   }
   const uint32_t items = std::max(std::max(p.n_obj * p.tiles, p.n_obj * p.edge_tiles),
                                   p.reconstruct ? p.n_obj : 0u);
-  const size_t lds = 2 * table_slot_bytes(K, F::kW);
+  return launch(decode_kernel<F, K, MODE, OCC, PLAIN, POL>, p, 2 * table_slot_bytes(K, F::kW),
+                items, stream);
+}
+
+template <class F, int K, int MODE>
+hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
   if constexpr (K == 10 && MODE == kDecode) {
-    // the benchmark configuration carries both register budgets
-    // (ECAMD_DEC_OCC=3 / 4, A/B in tools/ab_bench.py)
+    // the benchmark configuration carries the A/B variants
+    // (tools/ab_bench.py): ECAMD_DEC_OCC3=1 (3 waves per SIMD, no spills),
+    // ECAMD_DEC_PLAIN=1 (unaligned lane stores, no overlap lane)
+    const bool plain = env_flag("ECAMD_DEC_PLAIN", false);
+    switch (env_policy()) {
+      case 1:
+        return plain ? launch_decode_variant<F, K, MODE, kDecodeOcc, true, 1>(p, stream)
+                     : launch_decode_variant<F, K, MODE, kDecodeOcc, false, 1>(p, stream);
+      case 2:
+        return plain ? launch_decode_variant<F, K, MODE, kDecodeOcc, true, 2>(p, stream)
+                     : launch_decode_variant<F, K, MODE, kDecodeOcc, false, 2>(p, stream);
+      case 3:
+        return plain ? launch_decode_variant<F, K, MODE, kDecodeOcc, true, 3>(p, stream)
+                     : launch_decode_variant<F, K, MODE, kDecodeOcc, false, 3>(p, stream);
+      default:
+        break;
+    }
+    if (plain) return launch_decode_variant<F, K, MODE, kDecodeOcc, true>(p, stream);
     if (env_flag("ECAMD_DEC_OCC3", false))
-      return launch(decode_kernel<F, K, MODE, 3>, p, lds, items, stream);
+      return launch_decode_variant<F, K, MODE, 3, false>(p, stream);
   }
-  return launch(decode_kernel<F, K, MODE, kDecodeOcc>, p, lds, items, stream);
+  return launch_decode_variant<F, K, MODE, kDecodeOcc, false>(p, stream);
 }
 
 }  // namespace
