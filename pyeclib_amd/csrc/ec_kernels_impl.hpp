@@ -102,8 +102,9 @@ __device__ __forceinline__ Rsrc rsrc(const void* base, int records = -1) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  const int n = static_cast<int>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(records)));
   return __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, records, 0x00020000);
+      reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, n, 0x00020000);
 }
 // Cache policy of the interior streams (compile time; POL bits):
 // nontemporal by default, kPolLoadsCached / kPolStoresCached switch loads /
