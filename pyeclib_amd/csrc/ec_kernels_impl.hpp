@@ -964,11 +964,21 @@ inline int64_t last_room(uint32_t bs, uint64_t obj_len, uint32_t k) {
 }
 
 // Cache-policy variant requested through the environment (A/B of the
-// benchmark case only): ECAMD_LD_CACHED=1 / ECAMD_ST_CACHED=1.
-inline int env_policy() {
-  return (env_flag("ECAMD_LD_CACHED", false) ? kPolLoadsCached : 0) |
-         (env_flag("ECAMD_ST_CACHED", false) ? kPolStoresCached : 0);
+// benchmark case only): ECAMD_LD_CACHED=0/1, ECAMD_ST_CACHED=0/1.
+inline int env_policy(int dflt) {
+  return (env_flag("ECAMD_LD_CACHED", dflt & kPolLoadsCached) ? kPolLoadsCached : 0) |
+         (env_flag("ECAMD_ST_CACHED", dflt & kPolStoresCached) ? kPolStoresCached : 0);
 }
+
+// Defaults, measured on MI355X (round 2, tools/ab_bench.py, k=10 m=4,
+// 256 x 4 MiB): encode reads the object slices with the default cache
+// policy -- neighbouring slices share 128-B lines, which L2 then serves
+// twice (303 vs 308 us); stores stay nontemporal (cached: 331 us).
+// Decode stores each lane's 16 B where they belong (446 us) rather than
+// through the overlap-lane realignment (456 us): the 1008-B chunks it needs
+// cost 12 % more HBM reads and writes than the aligned units save.
+constexpr int kEncodePolicy = kPolLoadsCached;
+constexpr bool kDecodePlain = true;
 
 template <class F, int K, int NR>
 hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
@@ -979,11 +989,11 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   const uint32_t items = std::max(std::max(p.n_obj * p.tiles, p.n_obj * p.edge_tiles),
                                   p.headers ? p.n_obj : 0u);
   hipError_t e;
-  const int pol = (K == 10 && NR == 4) ? env_policy() : 0;
-  if (pol == 0)
-    e = launch(encode_kernel<F, K, NR, 0>, p, K * F::kTableBytes, items, stream);
+  const int pol = (K == 10 && NR == 4) ? env_policy(kEncodePolicy) : kEncodePolicy;
+  if (pol == kEncodePolicy)
+    e = launch(encode_kernel<F, K, NR, kEncodePolicy>, p, K * F::kTableBytes, items, stream);
   else if constexpr (K == 10 && NR == 4)
-    e = pol == 1   ? launch(encode_kernel<F, K, NR, 1>, p, K * F::kTableBytes, items, stream)
+    e = pol == 0   ? launch(encode_kernel<F, K, NR, 0>, p, K * F::kTableBytes, items, stream)
         : pol == 2 ? launch(encode_kernel<F, K, NR, 2>, p, K * F::kTableBytes, items, stream)
                    : launch(encode_kernel<F, K, NR, 3>, p, K * F::kTableBytes, items, stream);
   else
@@ -1038,8 +1048,8 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
     // the benchmark configuration carries the A/B variants
     // (tools/ab_bench.py): ECAMD_DEC_OCC3=1 (3 waves per SIMD, no spills),
     // ECAMD_DEC_PLAIN=1 (unaligned lane stores, no overlap lane)
-    const bool plain = env_flag("ECAMD_DEC_PLAIN", false);
-    switch (env_policy()) {
+    const bool plain = env_flag("ECAMD_DEC_PLAIN", kDecodePlain);
+    switch (env_policy(0)) {
       case 1:
         return plain ? launch_decode_variant<F, K, MODE, kDecodeOcc, true, 1>(p, stream)
                      : launch_decode_variant<F, K, MODE, kDecodeOcc, false, 1>(p, stream);
@@ -1052,11 +1062,11 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
       default:
         break;
     }
-    if (plain) return launch_decode_variant<F, K, MODE, kDecodeOcc, true>(p, stream);
+    if (!plain) return launch_decode_variant<F, K, MODE, kDecodeOcc, false>(p, stream);
     if (env_flag("ECAMD_DEC_OCC3", false))
-      return launch_decode_variant<F, K, MODE, 3, false>(p, stream);
+      return launch_decode_variant<F, K, MODE, 3, true>(p, stream);
   }
-  return launch_decode_variant<F, K, MODE, kDecodeOcc, false>(p, stream);
+  return launch_decode_variant<F, K, MODE, kDecodeOcc, kDecodePlain>(p, stream);
 }
 
 }  // namespace
