@@ -17,16 +17,18 @@
 // ds_read lane group can never hit one bank with two different addresses, so
 // every lookup is conflict-free whatever the data.
 //
-// Addressing (GF(2^16)).  Table [c][q][v] sits at byte 512c + 128q + 8v.  For
-// one input dword x (two symbols, eight nibbles) we build
-//   ylo = (x << 3) & 0x78787878               nibbles 0,2,4,6 scaled by 8
-//   yhi = ((x >> 1) & 0x78787878) | 0x80..80  nibbles 1,3,5,7 scaled by 8,
-//                                             +128 for odd q
-// and one v_perm_b32 per lookup assembles {y.byte_b, kb.byte} into the LDS
-// byte offset: kb carries the table set's LDS base >> 8 (plus 1 for nibble
-// positions 2-3); the per-input 512c lands in the ds_read immediate because
-// the input loop is unrolled over a compile-time k.  GF(2^8) is the same with
-// 128-B tables, 4-byte entries and one byte per symbol.
+// Addressing (GF(2^16)).  Table entry (c, q, v) sits at byte
+// 512c + 256(q >> 1) + 16v + 8(q & 1) (gf16.hpp), so the lookup address of
+// a nibble is the nibble times 16 plus a compile-time offset that rides in
+// the ds_read immediate (the input loop is unrolled over a compile-time k).
+// Byte b of an input dword x holds nibble positions q = 2(b & 1) and
+// 2(b & 1) + 1 of symbol b >> 1; their addresses are byte b of (x << 4)
+// and of x, masked with 0xF0.  Encode's tables sit at LDS 0, so one
+// v_and_b32_sdwa (src0_sel:BYTE_b) makes each address: 9 VALU ops for the
+// eight lookups of a dword.  Decode's table set lives in one of two slots,
+// so its addresses also carry the slot base: one v_perm_b32 per lookup
+// assembles {masked byte, base >> 8} (11 ops per dword).  GF(2^8) uses
+// 128-B tables, 4-byte entries, one byte per symbol and the v_perm form.
 //
 // Memory.  Each lane moves 16 B per input per step (global_load_dwordx4,
 // 1 KiB contiguous per wave-instruction); inputs are read once from HBM and
@@ -132,7 +134,25 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 
 // ---------------- GF(2^16): liberasurecode_rs_vand ----------------
 
-constexpr uint32_t kSel16[4] = {0x0C0C0400u, 0x0C0C0501u, 0x0C0C0402u, 0x0C0C0503u};
+// x & 0xF0 with x's byte B as the source operand (SDWA, gfx9): the
+// lookup address of the high nibble of byte B, times 16.
+#define ECAMD_SDWA_AND_BYTE(B)                                                              \
+  "v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_" #B \
+  " src1_sel:DWORD"
+template <int B>
+__device__ __forceinline__ uint32_t hi_nib16(uint32_t x) {
+  uint32_t r;
+  if constexpr (B == 0)
+    r = x & 0xF0u;
+  else if constexpr (B == 1)
+    asm(ECAMD_SDWA_AND_BYTE(1) : "=v"(r) : "v"(x), "v"(0xF0u));
+  else if constexpr (B == 2)
+    asm(ECAMD_SDWA_AND_BYTE(2) : "=v"(r) : "v"(x), "v"(0xF0u));
+  else
+    asm(ECAMD_SDWA_AND_BYTE(3) : "=v"(r) : "v"(x), "v"(0xF0u));
+  return r;
+}
+#undef ECAMD_SDWA_AND_BYTE
 
 // NW = 2: u64 entries (up to 4 rows); NW = 1: rows <= 2, read the low dword
 // only (ds_read_b32; same table layout).
@@ -143,9 +163,9 @@ struct Gf16 {
   struct Acc {
     uint2 s[8];  // s[2d] / s[2d+1]: rows 0-3 of the low / high symbol of input dword d
   };
-  static __device__ __forceinline__ uint32_t kb(uint32_t base) {
-    return (base >> 8) * 0x0101u + 0x0100u;
-  }
+  // second byte of a lookup address: the table set's LDS base (a multiple
+  // of 256, below 64 KiB)
+  static __device__ __forceinline__ uint32_t kb(uint32_t base) { return base >> 8; }
   static __device__ __forceinline__ void zero(Acc& a) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) a.s[i] = make_uint2(0, 0);
@@ -157,44 +177,63 @@ struct Gf16 {
 #pragma unroll
     for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(a.s[i].x), "+v"(a.s[i].y));
   }
+  // Lookup addresses of the 8 nibbles of x, in q order per symbol:
+  // a[4h + q] for symbol h (0 = low half-word).  Z: table set at LDS 0.
+  template <bool Z>
+  static __device__ __forceinline__ void addrs(uint32_t kb, uint32_t x, uint32_t (&a)[8]) {
+    const uint32_t w = x << 4;
+    if constexpr (Z) {
+      a[0] = hi_nib16<0>(w);
+      a[1] = hi_nib16<0>(x);
+      a[2] = hi_nib16<1>(w);
+      a[3] = hi_nib16<1>(x);
+      a[4] = hi_nib16<2>(w);
+      a[5] = hi_nib16<2>(x);
+      a[6] = hi_nib16<3>(w);
+      a[7] = hi_nib16<3>(x);
+    } else {
+      const uint32_t ml = w & 0xF0F0F0F0u, mh = x & 0xF0F0F0F0u;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        a[2 * b] = __builtin_amdgcn_perm(kb, ml, 0x0C0C0400u | b);
+        a[2 * b + 1] = __builtin_amdgcn_perm(kb, mh, 0x0C0C0400u | b);
+      }
+    }
+  }
+  // immediate offset of nibble position q inside an input's 512-B table
+  static constexpr uint32_t qoff(int q) { return 256u * (q >> 1) + 8u * (q & 1); }
+  template <bool Z>
   static __device__ __forceinline__ void mac_dword(uint32_t kb, uint32_t tab, uint32_t x,
                                                    uint2& s_lo, uint2& s_hi) {
-    const uint32_t ylo = (x << 3) & 0x78787878u;
-    const uint32_t yhi = ((x >> 1) & 0x78787878u) | 0x80808080u;
-    const uint32_t a0 = __builtin_amdgcn_perm(kb, ylo, kSel16[0]);
-    const uint32_t a1 = __builtin_amdgcn_perm(kb, yhi, kSel16[0]);
-    const uint32_t a2 = __builtin_amdgcn_perm(kb, ylo, kSel16[1]);
-    const uint32_t a3 = __builtin_amdgcn_perm(kb, yhi, kSel16[1]);
-    const uint32_t a4 = __builtin_amdgcn_perm(kb, ylo, kSel16[2]);
-    const uint32_t a5 = __builtin_amdgcn_perm(kb, yhi, kSel16[2]);
-    const uint32_t a6 = __builtin_amdgcn_perm(kb, ylo, kSel16[3]);
-    const uint32_t a7 = __builtin_amdgcn_perm(kb, yhi, kSel16[3]);
+    uint32_t a[8];
+    addrs<Z>(kb, x, a);
     if constexpr (NW == 2) {
-      const uint2 e0 = lds_u64(a0, tab), e1 = lds_u64(a1, tab), e2 = lds_u64(a2, tab),
-                  e3 = lds_u64(a3, tab);
-      const uint2 e4 = lds_u64(a4, tab), e5 = lds_u64(a5, tab), e6 = lds_u64(a6, tab),
-                  e7 = lds_u64(a7, tab);
+      const uint2 e0 = lds_u64(a[0], tab + qoff(0)), e1 = lds_u64(a[1], tab + qoff(1)),
+                  e2 = lds_u64(a[2], tab + qoff(2)), e3 = lds_u64(a[3], tab + qoff(3));
+      const uint2 e4 = lds_u64(a[4], tab + qoff(0)), e5 = lds_u64(a[5], tab + qoff(1)),
+                  e6 = lds_u64(a[6], tab + qoff(2)), e7 = lds_u64(a[7], tab + qoff(3));
       s_lo.x = xor3(xor3(s_lo.x, e0.x, e1.x), e2.x, e3.x);
       s_lo.y = xor3(xor3(s_lo.y, e0.y, e1.y), e2.y, e3.y);
       s_hi.x = xor3(xor3(s_hi.x, e4.x, e5.x), e6.x, e7.x);
       s_hi.y = xor3(xor3(s_hi.y, e4.y, e5.y), e6.y, e7.y);
     } else {
-      s_lo.x = xor3(xor3(s_lo.x, lds_u32(a0, tab), lds_u32(a1, tab)), lds_u32(a2, tab),
-                    lds_u32(a3, tab));
-      s_hi.x = xor3(xor3(s_hi.x, lds_u32(a4, tab), lds_u32(a5, tab)), lds_u32(a6, tab),
-                    lds_u32(a7, tab));
+      s_lo.x = xor3(xor3(s_lo.x, lds_u32(a[0], tab + qoff(0)), lds_u32(a[1], tab + qoff(1))),
+                    lds_u32(a[2], tab + qoff(2)), lds_u32(a[3], tab + qoff(3)));
+      s_hi.x = xor3(xor3(s_hi.x, lds_u32(a[4], tab + qoff(0)), lds_u32(a[5], tab + qoff(1))),
+                    lds_u32(a[6], tab + qoff(2)), lds_u32(a[7], tab + qoff(3)));
     }
   }
   // The scheduling barriers stop hipcc from hoisting every LDS lookup of the
   // unrolled input loop ahead of the XORs that consume them (2 VGPRs each).
+  template <bool Z = false>
   static __device__ __forceinline__ void mac(uint32_t kb, uint32_t tab, const uint4& x, Acc& a) {
-    mac_dword(kb, tab, x.x, a.s[0], a.s[1]);
+    mac_dword<Z>(kb, tab, x.x, a.s[0], a.s[1]);
     __builtin_amdgcn_sched_barrier(0);
-    mac_dword(kb, tab, x.y, a.s[2], a.s[3]);
+    mac_dword<Z>(kb, tab, x.y, a.s[2], a.s[3]);
     __builtin_amdgcn_sched_barrier(0);
-    mac_dword(kb, tab, x.z, a.s[4], a.s[5]);
+    mac_dword<Z>(kb, tab, x.z, a.s[4], a.s[5]);
     __builtin_amdgcn_sched_barrier(0);
-    mac_dword(kb, tab, x.w, a.s[6], a.s[7]);
+    mac_dword<Z>(kb, tab, x.w, a.s[6], a.s[7]);
     __builtin_amdgcn_sched_barrier(0);
   }
   static __device__ __forceinline__ uint32_t pack(const uint2& lo, const uint2& hi, int r) {
@@ -237,6 +276,7 @@ struct Gf8 {
                   lds_u32(__builtin_amdgcn_perm(kb, yhi, sel), tab));
     }
   }
+  template <bool Z = false>
   static __device__ __forceinline__ void mac(uint32_t kb, uint32_t tab, const uint4& x, Acc& a) {
     mac_dword(kb, tab, x.x, a.a + 0);
     __builtin_amdgcn_sched_barrier(0);
@@ -403,17 +443,29 @@ __device__ __forceinline__ void encode_load(const EncodeParams& p, uint32_t o, u
 // cur[j] waits only for cur's own loads (a branch around a load or store
 // makes it fall back to the shortest path's count -- measured in round 1 as
 // waiting for the prefetch too, which serialised memory and compute).
-template <class F, int K, int NR, int POL>
+template <class F, int K, int NR, int POL, bool SDWA, bool NOCOMP = false>
 __device__ __forceinline__ void encode_item(const EncodeParams& p, uint32_t w, uint32_t wn,
-                                            uint4 (&cur)[K], uint4 (&nxt)[K]) {
+                                            uint4 (&cur)[K], uint4 (&nxt)[K], bool none) {
   uint32_t o, x, on, xn;
   enc_item_pos(p, w, o, x);
   enc_item_pos(p, wn, on, xn);
-  encode_load<K, POL>(p, on, xn, nxt, wn == w);
+  encode_load<K, POL>(p, on, xn, nxt, none);
   typename F::Acc s;
   F::zero(s);
+  if constexpr (NOCOMP) {
+    // memory-only probe (A/B, wrong parity): the inputs XORed, no lookups
+    uint32_t* a = reinterpret_cast<uint32_t*>(&s);
 #pragma unroll
-  for (int j = 0; j < K; ++j) F::mac(F::kb(0), j * F::kTableBytes, cur[j], s);
+    for (int j = 0; j < K; ++j) {
+      a[0] ^= cur[j].x;
+      a[2] ^= cur[j].y;
+      a[4] ^= cur[j].z;
+      a[6] ^= cur[j].w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < K; ++j) F::template mac<SDWA>(F::kb(0), j * F::kTableBytes, cur[j], s);
+  }
   F::pin(s);
   const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
   const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x;
@@ -438,7 +490,7 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
   typename F::Acc s;
   F::zero(s);
 #pragma unroll
-  for (int j = 0; j < K; ++j) F::mac(F::kb(0), j * F::kTableBytes, x[j], s);
+  for (int j = 0; j < K; ++j) F::template mac<true>(F::kb(0), j * F::kTableBytes, x[j], s);
   F::pin(s);
   uint8_t* par = p.parity + static_cast<uint64_t>(o) * p.stripe_stride + p.row0 * p.frag_stride +
                  kHeaderBytes + t;
@@ -446,7 +498,9 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
   for (int q = 0; q < NR; ++q) store_partial(par + q * p.frag_stride, F::row(s, q), rem);
 }
 
-template <class F, int K, int NR, int POL>
+// SDWA = false: the table addresses are built with v_perm (decode's form;
+// A/B of the benchmark case, ECAMD_ENC_PERM=1).
+template <class F, int K, int NR, int POL, bool SDWA = true, bool NOCOMP = false>
 __global__ void __launch_bounds__(kThreadsPerBlock) encode_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
   if (p.headers != nullptr && p.row0 == 0)
@@ -471,14 +525,62 @@ __global__ void __launch_bounds__(kThreadsPerBlock) encode_kernel(EncodeParams p
     // two items per trip so cur / nxt stay compile-time register arrays
     while (true) {
       uint32_t wn = w + r.step < r.end ? w + r.step : w;
-      encode_item<F, K, NR, POL>(p, w, wn, xa, xb);
+      encode_item<F, K, NR, POL, SDWA, NOCOMP>(p, w, wn, xa, xb, wn == w);
       if (wn == w) break;
       w = wn;
       wn = w + r.step < r.end ? w + r.step : w;
-      encode_item<F, K, NR, POL>(p, w, wn, xb, xa);
+      encode_item<F, K, NR, POL, SDWA, NOCOMP>(p, w, wn, xb, xa, wn == w);
       if (wn == w) break;
       w = wn;
     }
+  }
+}
+
+// Prefetch depth 2 (A/B of the benchmark case, ECAMD_ENC_DEPTH2=1): while
+// item w is computed, items w + step and w + 2*step are in flight (three
+// register buffers; 3 waves per SIMD).
+template <class F, int K, int NR, int POL>
+__global__ void __launch_bounds__(kThreadsPerBlock) __attribute__((amdgpu_waves_per_eu(3, 8)))
+encode_kernel_d2(EncodeParams p) {
+  load_tables(p.tables, K * F::kTableBytes, 0);
+  if (p.headers != nullptr && p.row0 == 0)
+    for (uint32_t o = blockIdx.x; o < p.n_obj; o += gridDim.x) {
+      const uint64_t base = static_cast<uint64_t>(o) * p.stripe_stride;
+      block_headers(p.parity + base, p.frag_stride, p.headers + K * kHeaderBytes, p.m);
+      if (p.data != nullptr) block_headers(p.data + base, p.frag_stride, p.headers, K);
+    }
+  __syncthreads();
+  const uint32_t n_edge = p.n_obj * p.edge_tiles;
+  for (uint32_t e = gridDim.x - 1 - blockIdx.x; e < n_edge; e += gridDim.x)
+    encode_edge_item<F, K, NR>(p, e);
+  const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
+  uint32_t w = r.begin;
+  if (w >= r.end) return;
+  uint4 xa[K], xb[K], xc[K];
+  // item w + k*step if it exists, else w itself (loaded through a
+  // zero-record descriptor: no traffic)
+  auto ahead = [&](uint32_t v, uint32_t k) { return v + k * r.step < r.end ? v + k * r.step : v; };
+  {
+    uint32_t o, x;
+    enc_item_pos(p, w, o, x);
+    encode_load<K, POL>(p, o, x, xa);
+    const uint32_t w1 = ahead(w, 1);
+    enc_item_pos(p, w1, o, x);
+    encode_load<K, POL>(p, o, x, xb, w1 == w);
+  }
+  while (true) {
+    uint32_t f = ahead(w, 2);
+    encode_item<F, K, NR, POL, true>(p, w, f, xa, xc, f == w);
+    if (w + r.step >= r.end) break;
+    w += r.step;
+    f = ahead(w, 2);
+    encode_item<F, K, NR, POL, true>(p, w, f, xb, xa, f == w);
+    if (w + r.step >= r.end) break;
+    w += r.step;
+    f = ahead(w, 2);
+    encode_item<F, K, NR, POL, true>(p, w, f, xc, xb, f == w);
+    if (w + r.step >= r.end) break;
+    w += r.step;
   }
 }
 
@@ -554,8 +656,10 @@ __device__ __forceinline__ void table_prefetch(const DecodeParams& p, uint32_t t
   pre.table = table;
 }
 
-// Make d's table set current; returns its kb.  Block-uniform (barrier).
-template <class F, int K, class D>
+// Make d's table set current; returns its kb.  Block-uniform (barrier;
+// SYNC: a barrier even when the set is unchanged -- the staged stores'
+// write-after-read fence on the staging area).
+template <class F, int K, bool SYNC = false, class D>
 __device__ __forceinline__ uint32_t ensure_tables(const DecodeParams& p, const D& d, Slots& st,
                                                   const TablePre<F, K>& pre) {
   constexpr uint32_t kSlot = table_slot_bytes(K, F::kW);
@@ -582,6 +686,8 @@ __device__ __forceinline__ uint32_t ensure_tables(const DecodeParams& p, const D
     }
     __syncthreads();
     st.table = d.table();
+  } else if constexpr (SYNC) {
+    __syncthreads();
   }
   return F::kb(st.slot * kSlot);
 }
@@ -719,6 +825,89 @@ __device__ __forceinline__ void st_unit(Rsrc out, uint32_t vst, uint32_t soff, c
   buf_st<CACHED>(out, vst, soff - s, u);
 }
 
+// Staged object stores (STAGED, kDecode).  The block's four waves hold the
+// 4 KiB tile [t0, t0 + 4096) of every slice; they write it to LDS (slice c
+// at stage + c * 4096), and after a barrier thread u stores the 16-B-aligned
+// object unit u of each slice: slice j's tile lands at A = j*bs + t0, so with
+// a = A mod 16 unit u covers tile bytes [16u - a, 16u - a + 16) -- the last
+// a bytes of staged unit u - 1 and the first 16 - a of unit u (two aligned
+// ds_read_b128 and a funnel shift).  Every store is a whole aligned 16-B
+// unit except the two at the tile's ends (unit 0: bytes [a, 16); unit 256:
+// bytes [0, a)), so a slice's lines are split only where two tiles meet
+// (every 4 KiB), not at every wave's 1 KiB as with lane-natural stores.
+constexpr uint32_t kStageTile = kWavesPerBlock * kChunkBytes;  // 4096
+
+// Bytes [lo, hi) of v stored at voff + lo (naturally aligned pieces).
+__device__ __forceinline__ void buf_st_bytes(Rsrc r, uint32_t voff, const uint4& v, uint32_t lo,
+                                             uint32_t hi) {
+  const uint64_t q0 = v.x | (static_cast<uint64_t>(v.y) << 32);
+  const uint64_t q1 = v.z | (static_cast<uint64_t>(v.w) << 32);
+  for (uint32_t i = lo; i < hi;) {
+    const uint64_t qv = i < 8 ? q0 >> (8 * i) : q1 >> (8 * (i - 8));
+    if ((i & 7) == 0 && i + 8 <= hi) {
+      v2u d;
+      d.x = static_cast<uint32_t>(qv);
+      d.y = static_cast<uint32_t>(qv >> 32);
+      __builtin_amdgcn_raw_buffer_store_b64(d, r, voff + i, 0, 0);
+      i += 8;
+    } else if ((i & 3) == 0 && i + 4 <= hi) {
+      __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(qv), r, voff + i, 0, 0);
+      i += 4;
+    } else if ((i & 1) == 0 && i + 2 <= hi) {
+      __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(qv), r, voff + i, 0, 0);
+      i += 2;
+    } else {
+      __builtin_amdgcn_raw_buffer_store_b8(static_cast<unsigned char>(qv), r, voff + i, 0, 0);
+      i += 1;
+    }
+  }
+}
+
+// Bytes [b0, b0 + 16) of the 32-byte pair (lo, hi), b0 = 16 - a in 1..15
+// (wave-uniform).
+__device__ __forceinline__ uint4 funnel16(const uint4& lo, const uint4& hi, uint32_t b0) {
+  const uint32_t r = b0 & 3u;
+  switch (b0 >> 2) {
+    case 0:
+      return make_uint4(__builtin_amdgcn_alignbyte(lo.y, lo.x, r), __builtin_amdgcn_alignbyte(lo.z, lo.y, r),
+                        __builtin_amdgcn_alignbyte(lo.w, lo.z, r), __builtin_amdgcn_alignbyte(hi.x, lo.w, r));
+    case 1:
+      return make_uint4(__builtin_amdgcn_alignbyte(lo.z, lo.y, r), __builtin_amdgcn_alignbyte(lo.w, lo.z, r),
+                        __builtin_amdgcn_alignbyte(hi.x, lo.w, r), __builtin_amdgcn_alignbyte(hi.y, hi.x, r));
+    case 2:
+      return make_uint4(__builtin_amdgcn_alignbyte(lo.w, lo.z, r), __builtin_amdgcn_alignbyte(hi.x, lo.w, r),
+                        __builtin_amdgcn_alignbyte(hi.y, hi.x, r), __builtin_amdgcn_alignbyte(hi.z, hi.y, r));
+    default:
+      return make_uint4(__builtin_amdgcn_alignbyte(hi.x, lo.w, r), __builtin_amdgcn_alignbyte(hi.y, hi.x, r),
+                        __builtin_amdgcn_alignbyte(hi.z, hi.y, r), __builtin_amdgcn_alignbyte(hi.w, hi.z, r));
+  }
+}
+
+// Store one staged slice tile (LDS bytes [sb, sb + 4096), preceded by 16
+// readable bytes) at object offset A.  Block-wide; after the staging barrier.
+template <bool CACHED>
+__device__ __forceinline__ void stage_out(Rsrc out, uint32_t sb, uint32_t A) {
+  const uint32_t u = threadIdx.x;
+  const uint32_t a = A & 15u, U0 = A - a;
+  const v4u c = *lds_v4(sb + 16 * u);
+  const uint4 cu = make_uint4(c.x, c.y, c.z, c.w);
+  if (a == 0) {
+    buf_st<CACHED>(out, 16 * u, U0, cu);
+    return;
+  }
+  const v4u p = *lds_v4(sb + 16 * u - 16);
+  const uint4 v = funnel16(make_uint4(p.x, p.y, p.z, p.w), cu, 16 - a);
+  if (u != 0)
+    buf_st<CACHED>(out, 16 * u, U0, v);
+  else
+    buf_st_bytes(out, U0, v, a, 16);
+  if (u == kThreadsPerBlock - 1) {
+    // unit 256: the last a bytes of staged unit 255
+    const uint4 t = funnel16(cu, make_uint4(0, 0, 0, 0), 16 - a);
+    buf_st_bytes(out, U0 + 16 * kThreadsPerBlock, t, 0, a);
+  }
+}
+
 // kDecode: the k inputs are the first k available fragments in ascending
 // order, so the present data fragments come first and the parity inputs --
 // as many as there are missing data slices, e -- are the last e.  After the
@@ -747,7 +936,7 @@ __device__ __forceinline__ void place_rows(const typename F::Acc& s, uint32_t e,
 
 // One interior decode / reconstruct item with inputs in `cur`; prefetches the
 // block's next item (payloads into `nxt`, its table set into `pre`).
-template <class F, int K, int MODE, bool PLAIN, int POL>
+template <class F, int K, int MODE, bool PLAIN, int POL, bool STAGED, bool NOCOMP = false>
 __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, uint32_t wn,
                                             Slots& st, TablePre<F, K>& pre, uint4 (&cur)[K],
                                             uint4 (&nxt)[K]) {
@@ -757,13 +946,13 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
   const DescU dn = load_desc(p, on);
   decode_load<K, POL>(p, on, dn, xn, nxt, wn == w);
   const DescU d = load_desc(p, o);
-  const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
+  const uint32_t kb = ensure_tables<F, K, STAGED>(p, d, st, pre);
   if (dn.n_out() != 0 && dn.table() != st.table && dn.table() != pre.table)
     table_prefetch<F, K>(p, dn.table(), pre);
   const uint32_t n_out = d.n_out();
   typename F::Acc s;
   F::zero(s);
-  if (n_out != 0) {
+  if (!NOCOMP && n_out != 0) {
 #pragma unroll
     for (int j = 0; j < K; ++j) F::mac(kb, j * F::kTableBytes, cur[j], s);
   }
@@ -783,7 +972,25 @@ __device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, u
       else
         st_unit<kStC>(out, vst, off + x, v, off & 15u);
     };
-    if constexpr (MODE == kDecode) {
+    if constexpr (MODE == kDecode && STAGED) {
+      place_rows<F, K>(s, n_out, cur);
+      constexpr uint32_t sb0 = 2 * table_slot_bytes(K, F::kW) + 16;
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        v4u v;
+        v.x = cur[j].x;
+        v.y = cur[j].y;
+        v.z = cur[j].z;
+        v.w = cur[j].w;
+        *lds_v4(sb0 + j * kStageTile + wave_in_block() * kChunkBytes + lane_id() * 16) = v;
+      }
+      __syncthreads();
+      const uint32_t t0 = x - wave_in_block() * kChunkBytes;
+      const Rsrc outb = rsrc(outp);
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        stage_out<kStC>(outb, sb0 + j * kStageTile, slice_of(d, n_out, K, j) * p.bs + t0);
+    } else if constexpr (MODE == kDecode) {
       place_rows<F, K>(s, n_out, cur);
 #pragma unroll
       for (int j = 0; j < K; ++j) put(slice_of(d, n_out, K, j) * p.bs, cur[j]);
@@ -866,7 +1073,8 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
 // OCC = minimum waves per SIMD the register allocation must allow (hipcc
 // left alone spends ~140 VGPRs on the decode variants: 3 waves per SIMD; 4
 // fits in 128 VGPRs with a few spills around the table prefetch).
-template <class F, int K, int MODE, int OCC, bool PLAIN, int POL>
+template <class F, int K, int MODE, int OCC, bool PLAIN, int POL, bool STAGED = false,
+          bool NOCOMP = false>
 __global__ void __launch_bounds__(kThreadsPerBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8)))
 decode_kernel(DecodeParams p) {
   if (MODE == kReconstruct && p.headers != nullptr)
@@ -891,11 +1099,11 @@ decode_kernel(DecodeParams p) {
     if (d0.n_out() != 0 && d0.table() != st.table) table_prefetch<F, K>(p, d0.table(), pre);
     while (true) {
       uint32_t wn = w + r.step < r.end ? w + r.step : w;
-      decode_item<F, K, MODE, PLAIN, POL>(p, w, wn, st, pre, xa, xb);
+      decode_item<F, K, MODE, PLAIN, POL, STAGED, NOCOMP>(p, w, wn, st, pre, xa, xb);
       if (wn == w) break;
       w = wn;
       wn = w + r.step < r.end ? w + r.step : w;
-      decode_item<F, K, MODE, PLAIN, POL>(p, w, wn, st, pre, xb, xa);
+      decode_item<F, K, MODE, PLAIN, POL, STAGED, NOCOMP>(p, w, wn, st, pre, xb, xa);
       if (wn == w) break;
       w = wn;
     }
@@ -979,6 +1187,7 @@ inline int env_policy(int dflt) {
 // cost 12 % more HBM reads and writes than the aligned units save.
 constexpr int kEncodePolicy = kPolLoadsCached;
 constexpr bool kDecodePlain = true;
+constexpr bool kDecodeStaged = false;
 
 template <class F, int K, int NR>
 hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
@@ -988,9 +1197,24 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   p.edge_tiles = (p.bs + tile - 1) / tile - p.tiles;
   const uint32_t items = std::max(std::max(p.n_obj * p.tiles, p.n_obj * p.edge_tiles),
                                   p.headers ? p.n_obj : 0u);
-  hipError_t e;
+  hipError_t e = hipErrorInvalidValue;
   const int pol = (K == 10 && NR == 4) ? env_policy(kEncodePolicy) : kEncodePolicy;
-  if (pol == kEncodePolicy)
+  bool sdwa = true;
+  if constexpr (K == 10 && NR == 4) sdwa = !env_flag("ECAMD_ENC_PERM", false);
+  if constexpr (K == 10 && NR == 4) {
+    if (pol == kEncodePolicy && env_flag("ECAMD_ENC_NOCOMP", false))
+      return launch(encode_kernel<F, K, NR, kEncodePolicy, true, true>, p, K * F::kTableBytes,
+                    items, stream);
+    if (pol == kEncodePolicy && env_flag("ECAMD_ENC_DEPTH2", false)) {
+      e = launch(encode_kernel_d2<F, K, NR, kEncodePolicy>, p, K * F::kTableBytes, items, stream);
+      if (e != hipSuccess || p.data == nullptr || p.row0 != 0) return e;
+      return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + tile - 1) / tile), stream);
+    }
+  }
+  if (pol == kEncodePolicy && !sdwa) {
+    if constexpr (K == 10 && NR == 4)
+      e = launch(encode_kernel<F, K, NR, kEncodePolicy, false>, p, K * F::kTableBytes, items, stream);
+  } else if (pol == kEncodePolicy)
     e = launch(encode_kernel<F, K, NR, kEncodePolicy>, p, K * F::kTableBytes, items, stream);
   else if constexpr (K == 10 && NR == 4)
     e = pol == 0   ? launch(encode_kernel<F, K, NR, 0>, p, K * F::kTableBytes, items, stream)
@@ -1020,7 +1244,20 @@ hipError_t launch_encode_rows(const EncodeParams& p, hipStream_t stream) {
 
 constexpr int kDecodeOcc = 4;
 
-template <class F, int K, int MODE, int OCC, bool PLAIN, int POL = 0>
+// LDS of a decode launch: two table slots (+ the staging area).
+template <class F, int K, bool STAGED>
+constexpr uint32_t decode_lds_bytes() {
+  return 2 * table_slot_bytes(K, F::kW) + (STAGED ? 16 + K * kStageTile : 0);
+}
+// Staged stores need K * 4 KiB of LDS per block; used while two blocks per
+// CU still fit (k <= 16 for GF(2^16)).
+template <class F, int K>
+constexpr bool staged_fits() {
+  return decode_lds_bytes<F, K, true>() <= 80u * 1024u;
+}
+
+template <class F, int K, int MODE, int OCC, bool PLAIN, int POL = 0, bool STAGED = false,
+          bool NOCOMP = false>
 hipError_t launch_decode_variant(DecodeParams p, hipStream_t stream) {
   constexpr uint32_t tile = kWavesPerBlock * chunk_stride<MODE, PLAIN>();
   if constexpr (!overlaps<MODE, PLAIN>()) {
@@ -1038,12 +1275,24 @@ hipError_t launch_decode_variant(DecodeParams p, hipStream_t stream) {
   }
   const uint32_t items = std::max(std::max(p.n_obj * p.tiles, p.n_obj * p.edge_tiles),
                                   p.reconstruct ? p.n_obj : 0u);
-  return launch(decode_kernel<F, K, MODE, OCC, PLAIN, POL>, p, 2 * table_slot_bytes(K, F::kW),
-                items, stream);
+  return launch(decode_kernel<F, K, MODE, OCC, PLAIN, POL, STAGED, NOCOMP>, p,
+                decode_lds_bytes<F, K, STAGED>(), items, stream);
 }
 
 template <class F, int K, int MODE>
 hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
+  if constexpr (K == 10 && MODE == kDecode) {
+    if (env_flag("ECAMD_DEC_NOCOMP", false))  // memory-only probe (wrong output)
+      return env_flag("ECAMD_DEC_STAGED", kDecodeStaged)
+                 ? launch_decode_variant<F, K, MODE, 3, true, 0, true, true>(p, stream)
+                 : launch_decode_variant<F, K, MODE, kDecodeOcc, true, 0, false, true>(p, stream);
+  }
+  if constexpr (MODE == kDecode && staged_fits<F, K>()) {
+    // staged, line-friendly object stores (LDS bounds occupancy to 3 blocks
+    // per CU at k = 10, so the register budget is 3 waves per SIMD)
+    if (env_flag("ECAMD_DEC_STAGED", kDecodeStaged))
+      return launch_decode_variant<F, K, MODE, 3, true, 0, true>(p, stream);
+  }
   if constexpr (K == 10 && MODE == kDecode) {
     // the benchmark configuration carries the A/B variants
     // (tools/ab_bench.py): ECAMD_DEC_OCC3=1 (3 waves per SIMD, no spills),

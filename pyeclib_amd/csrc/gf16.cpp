@@ -82,7 +82,7 @@ void build_nibble_tables(const uint16_t* rows, int nrows, int ncols, uint64_t* o
         const uint16_t x = static_cast<uint16_t>(v << (4 * q));
         for (int r = 0; r < nrows && r < 4; ++r)
           e |= static_cast<uint64_t>(gf.mul(rows[r * ncols + c], x)) << (16 * r);
-        out[(c * 4 + q) * 16 + v] = e;
+        out[c * 64 + (q >> 1) * 32 + v * 2 + (q & 1)] = e;
       }
 }
 

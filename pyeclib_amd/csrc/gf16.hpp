@@ -54,10 +54,14 @@ bool invert(const GfMatrix& a, GfMatrix& out, int n);
 // Nibble lookup tables for the GPU region kernel.
 //
 // For an R x C coefficient matrix M (R <= 4 rows per table set), entry
-// [c][q][v] (u64) packs the four 16-bit products M[r][c] * (v << 4q) for
-// r = 0..3 (zero for r >= R) at bits 16r..16r+15.  One table set is C * 512 B.
-// Because multiplication by a constant is GF(2)-linear,
-//   M[r][c] * x = XOR_q entry[c][q][nibble_q(x)].r
+// (c, q, v) (u64) packs the four 16-bit products M[r][c] * (v << 4q) for
+// r = 0..3 (zero for r >= R) at bits 16r..16r+15.  Because multiplication by
+// a constant is GF(2)-linear,
+//   M[r][c] * x = XOR_q entry(c, q, nibble_q(x)).r
+// Layout [c][q >> 1][v][q & 1]: entry (c, q, v) at byte
+// 512c + 256(q >> 1) + 16v + 8(q & 1), so the lookup address of a nibble is
+// that nibble times 16 -- a byte of the input masked with 0xF0 -- plus a
+// compile-time offset (ec_kernels_impl.hpp).  One table set is C * 512 B.
 void build_nibble_tables(const uint16_t* rows, int nrows, int ncols, uint64_t* out);
 
 }  // namespace ecamd

@@ -46,11 +46,11 @@ for s in $STEPS; do
     (cd /tmp && timeout -k 10 120 rocprofv3 -L > $O/counters.txt 2>&1) || true
     grep -c . $O/counters.txt ;;
   sq)
-    for f in pmc1 pmc2 pmc3; do
+    for f in ${SQ_FILES:-pmc1 pmc2 pmc3}; do
       (cd /tmp && timeout -s KILL 150 rocprofv3 -i $R/tools/$f.txt --output-format csv -d $O/sq_$f -o run \
         -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host > $O/sq_$f.log 2>&1)
     done
-    python3 $R/tools/pmc_table.py $O/sq_pmc1 $O/sq_pmc2 $O/sq_pmc3 > $O/sq_table.txt 2>&1 || true
+    python3 $R/tools/pmc_table.py $(for f in ${SQ_FILES:-pmc1 pmc2 pmc3}; do echo $O/sq_$f; done) > $O/sq_table.txt 2>&1 || true
     cat $O/sq_table.txt ;;
   *) echo "unknown step $s"; exit 2 ;;
   esac
