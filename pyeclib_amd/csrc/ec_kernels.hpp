@@ -40,10 +40,9 @@ __host__ __device__ constexpr uint32_t table_slot_bytes(uint32_t k, uint32_t w) 
 }
 
 // ECAMD_XCD=0 turns off the XCD-major work split (every kernel).
-// A/B variants of the benchmark case (k = 10), chosen from the environment
-// at each launch so tools/ab_bench.py can compare them in one process:
-// ECAMD_LD_CACHED=1 / ECAMD_ST_CACHED=1 (default cache policy instead of
-// nontemporal), ECAMD_DEC_PLAIN=1, ECAMD_DEC_OCC3=1 (ec_kernels_impl.hpp).
+// ECAMD_ENC_NOCOMP=1 / ECAMD_DEC_NOCOMP=1: memory-only probes of the
+// benchmark case (k = 10; wrong output), read at each launch so
+// tools/ab_bench.py can time them beside the real kernels in one process.
 
 struct EncodeParams {
   const uint8_t* objs;      // object o at objs + o * obj_stride

@@ -34,8 +34,8 @@
 // 1 KiB contiguous per wave-instruction); inputs are read once from HBM and
 // every output byte is written once.  Fragment payloads inside an object
 // start at j*bs, which is only 2-byte (GF(2^16)) or 1-byte aligned: encode
-// reads those slices with gfx9's unaligned loads; decode writes them as
-// realigned 16-B units (see "Realigned object stores").
+// reads those slices with gfx9's unaligned loads and decode writes them with
+// unaligned stores (see "Object stores").
 #pragma once
 
 #include <algorithm>
@@ -108,15 +108,25 @@ __device__ __forceinline__ Rsrc rsrc(const void* base, int records = -1) {
   return __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, n, 0x00020000);
 }
-// Cache policy of the interior streams (compile time; POL bits):
-// nontemporal by default, kPolLoadsCached / kPolStoresCached switch loads /
-// stores to the default policy (A/B variants of the benchmark case).
-constexpr int kPolLoadsCached = 1, kPolStoresCached = 2;
+// CACHED: default cache policy instead of nontemporal.
 template <bool CACHED = false>
 __device__ __forceinline__ uint4 buf_ld(Rsrc r, uint32_t voff, uint32_t soff) {
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, CACHED ? 0 : kNt);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// One wait state after a 16-B buffer store.  Measured on MI355X (round 2):
+// a `buffer_store_dwordx4 v[30:33], v52, s[24:27], s31 offen` directly
+// followed by a VALU write of v30 stored a wrong first dword.  hipcc's hazard
+// recognizer only guards stores of > 8 bytes whose soffset is NOT an SGPR, so
+// every store here gets its own wait state (the sched barriers keep the
+// s_nop directly behind the store); tools/store_hazard.py checks the
+// generated code.
+__device__ __forceinline__ void st_fence() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 0");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 template <bool CACHED = false>
 __device__ __forceinline__ void buf_st(Rsrc r, uint32_t voff, uint32_t soff, const uint4& x) {
   v4u v;
@@ -125,6 +135,7 @@ __device__ __forceinline__ void buf_st(Rsrc r, uint32_t voff, uint32_t soff, con
   v.z = x.z;
   v.w = x.w;
   __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, soff, CACHED ? 0 : kNt);
+  st_fence();
 }
 
 // a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
@@ -159,6 +170,7 @@ __device__ __forceinline__ uint32_t hi_nib16(uint32_t x) {
 template <int NW>
 struct Gf16 {
   static constexpr uint32_t kW = 16;
+  static constexpr int kRows = NW == 2 ? 4 : 2;  // output rows one table entry carries
   static constexpr uint32_t kTableBytes = 512;
   struct Acc {
     uint2 s[8];  // s[2d] / s[2d+1]: rows 0-3 of the low / high symbol of input dword d
@@ -223,10 +235,39 @@ struct Gf16 {
                     lds_u32(a[6], tab + qoff(2)), lds_u32(a[7], tab + qoff(3)));
     }
   }
+  // One symbol (h = 0: low half-word) of x at a time: half the lookup
+  // temporaries of mac_dword live at once (register-lean kernels).
+  template <bool Z>
+  static __device__ __forceinline__ void mac_dword_split(uint32_t kb, uint32_t tab, uint32_t x,
+                                                         uint2& s_lo, uint2& s_hi) {
+    uint32_t a[8];
+    addrs<Z>(kb, x, a);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint2& s = h ? s_hi : s_lo;
+      if constexpr (NW == 2) {
+        const uint2 e0 = lds_u64(a[4 * h], tab + qoff(0)), e1 = lds_u64(a[4 * h + 1], tab + qoff(1)),
+                    e2 = lds_u64(a[4 * h + 2], tab + qoff(2)), e3 = lds_u64(a[4 * h + 3], tab + qoff(3));
+        s.x = xor3(xor3(s.x, e0.x, e1.x), e2.x, e3.x);
+        s.y = xor3(xor3(s.y, e0.y, e1.y), e2.y, e3.y);
+      } else {
+        s.x = xor3(xor3(s.x, lds_u32(a[4 * h], tab + qoff(0)), lds_u32(a[4 * h + 1], tab + qoff(1))),
+                   lds_u32(a[4 * h + 2], tab + qoff(2)), lds_u32(a[4 * h + 3], tab + qoff(3)));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
   // The scheduling barriers stop hipcc from hoisting every LDS lookup of the
   // unrolled input loop ahead of the XORs that consume them (2 VGPRs each).
-  template <bool Z = false>
+  template <bool Z = false, bool SPLIT = false>
   static __device__ __forceinline__ void mac(uint32_t kb, uint32_t tab, const uint4& x, Acc& a) {
+    if constexpr (SPLIT) {
+      mac_dword_split<Z>(kb, tab, x.x, a.s[0], a.s[1]);
+      mac_dword_split<Z>(kb, tab, x.y, a.s[2], a.s[3]);
+      mac_dword_split<Z>(kb, tab, x.z, a.s[4], a.s[5]);
+      mac_dword_split<Z>(kb, tab, x.w, a.s[6], a.s[7]);
+      return;
+    }
     mac_dword<Z>(kb, tab, x.x, a.s[0], a.s[1]);
     __builtin_amdgcn_sched_barrier(0);
     mac_dword<Z>(kb, tab, x.y, a.s[2], a.s[3]);
@@ -252,6 +293,7 @@ struct Gf16 {
 
 struct Gf8 {
   static constexpr uint32_t kW = 8;
+  static constexpr int kRows = 4;
   static constexpr uint32_t kTableBytes = 128;  // [q 0..1][v 0..15] u32
   struct Acc {
     uint32_t a[16];  // a[4d + b]: rows 0-3 (bytes 0-3) for byte b of input dword d
@@ -276,7 +318,7 @@ struct Gf8 {
                   lds_u32(__builtin_amdgcn_perm(kb, yhi, sel), tab));
     }
   }
-  template <bool Z = false>
+  template <bool Z = false, bool SPLIT = false>
   static __device__ __forceinline__ void mac(uint32_t kb, uint32_t tab, const uint4& x, Acc& a) {
     mac_dword(kb, tab, x.x, a.a + 0);
     __builtin_amdgcn_sched_barrier(0);
@@ -358,18 +400,14 @@ __device__ __forceinline__ int64_t object_bytes(uint32_t idx, uint32_t bs, uint3
 
 // ---------------- work decomposition ----------------
 //
-// Work item = (object o, tile): the block's 4 waves each take one chunk of
-// consecutive payload positions of object o.  Encode and reconstruct chunks
-// are 1 KiB (64 lanes x 16 B; tile = 4 KiB).  Decode chunks advance 1008 B:
-// lane 0 re-reads the previous chunk's last 16 B (the "overlap lane") so that
-// lanes 1..63 can assemble 16-B-aligned object units (see "Realigned object
-// stores"); tile = 4032 B.  Tiles [0, tiles) of every object are "interior":
-// every lane reads 16 in-bounds bytes from every input and writes one
-// 16-byte unit to every output, so they run unconditionally, unrolled over K
-// and with the next item's loads in flight (register double buffering).  The
-// rest of each payload -- the head and tail of decode's object slices, the
-// payload tail, the zero padding -- are "edge" items (4 KiB each, per-lane
-// byte bounds), run first by the highest-numbered blocks.
+// Work item = (object o, tile): the block's 4 waves each take one 1 KiB chunk
+// (64 lanes x 16 B) of consecutive payload positions of object o; tile =
+// 4 KiB.  Tiles [0, tiles) of every object are "interior": every lane reads
+// 16 in-bounds bytes from every input and writes one 16-byte unit to every
+// output, so they run unconditionally, unrolled over K, as a stream (see
+// "streaming").  The rest of each payload -- the tails of decode's object
+// slices, the payload tail, the zero padding -- are "edge" items (4 KiB
+// each, per-lane byte bounds) in a launch of their own.
 //
 // Order (measured, round 2: tools/ab_bench.py): the waves of the grid must
 // work on one compact region of memory at a time -- blocks walk the item list
@@ -416,62 +454,47 @@ __device__ __forceinline__ void store_window(uint8_t* base, uint32_t pos, const 
     put_bytes(base + pos + a, v, static_cast<uint32_t>(a), static_cast<uint32_t>(b - a));
 }
 
+// ---------------- streaming ----------------
+//
+// Every interior loop streams its inputs: a wave keeps NB input chunks
+// (16 B per lane each) in flight continuously.  The products of input j are
+// taken as soon as its chunk has arrived, and its registers are immediately
+// refilled with input j + NB -- past the item's last input the stream moves
+// on to the block's next item (through a zero-record descriptor after the
+// last item: no traffic).  A wave therefore needs NB x 16 B of input
+// registers instead of a whole item double-buffered (2K x 16 B), so 6-8 waves
+// per SIMD fit, and memory and the table lookups overlap across them.  NB
+// divides K so every item uses the registers in the same order (the loop body
+// is one item, unrolled over K, with exact s_waitcnt counts: no memory
+// instruction sits behind a branch).
+//
+// Measured (round 2, tools/ab_bench.py, k = 10, m = 4, 256 x 4 MiB, same
+// process): encode 284.4 -> 274.3 us, decode 453.3 -> 436.6 us against the
+// previous register double-buffered kernels (4 waves per SIMD, spills in the
+// decode loop).
+template <int K>
+__host__ __device__ constexpr int stream_bufs() {
+  for (int d = 6; d >= 2; --d)
+    if (K % d == 0) return d;
+  return K;
+}
+
+// Waves per SIMD the streaming kernels are built for (register budget) and
+// launched at (blocks per CU; each block has one wave per SIMD).  Decode runs
+// fewer blocks than its budget allows: 4 per CU measured best at k = 10
+// (436.6 us vs 450.5 at 6 and 475.2 at 8).
+constexpr int kEncodeOcc = 8, kEncodePerCu = 8;
+constexpr int kDecodeOcc = 6, kDecodePerCu = 4;
+
 // ---------------- encode ----------------
 
 // Interior item w: 4 KiB of payload positions starting at t0 = tile*4096;
 // this wave's chunk at t0 + 1024*wave, the lane at + 16*lane (voffset).
+constexpr uint32_t kTile = kWavesPerBlock * kChunkBytes;
 __device__ __forceinline__ void enc_item_pos(const EncodeParams& p, uint32_t w, uint32_t& o,
                                              uint32_t& x) {
   o = w / p.tiles;
-  x = (w - o * p.tiles) * (kWavesPerBlock * kChunkBytes) + wave_in_block() * kChunkBytes;
-}
-
-template <int K, int POL>
-__device__ __forceinline__ void encode_load(const EncodeParams& p, uint32_t o, uint32_t x,
-                                            uint4 (&v)[K], bool none = false) {
-  const Rsrc r = rsrc(p.objs + static_cast<uint64_t>(o) * p.obj_stride, none ? 0 : -1);
-#pragma unroll
-  for (int j = 0; j < K; ++j)
-    v[j] = buf_ld<(POL & kPolLoadsCached) != 0>(r, lane_id() * 16, j * p.bs + x);
-}
-
-// One interior item with its inputs in `cur`; first issues the loads of the
-// block's next item into `nxt` so they are in flight while this item's table
-// lookups run (the last item's "next" loads go through a zero-record
-// descriptor: no memory traffic).  Every memory
-// operation in the loop body is unconditional, so hipcc's s_waitcnt before
-// cur[j] waits only for cur's own loads (a branch around a load or store
-// makes it fall back to the shortest path's count -- measured in round 1 as
-// waiting for the prefetch too, which serialised memory and compute).
-template <class F, int K, int NR, int POL, bool SDWA, bool NOCOMP = false>
-__device__ __forceinline__ void encode_item(const EncodeParams& p, uint32_t w, uint32_t wn,
-                                            uint4 (&cur)[K], uint4 (&nxt)[K], bool none) {
-  uint32_t o, x, on, xn;
-  enc_item_pos(p, w, o, x);
-  enc_item_pos(p, wn, on, xn);
-  encode_load<K, POL>(p, on, xn, nxt, none);
-  typename F::Acc s;
-  F::zero(s);
-  if constexpr (NOCOMP) {
-    // memory-only probe (A/B, wrong parity): the inputs XORed, no lookups
-    uint32_t* a = reinterpret_cast<uint32_t*>(&s);
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      a[0] ^= cur[j].x;
-      a[2] ^= cur[j].y;
-      a[4] ^= cur[j].z;
-      a[6] ^= cur[j].w;
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < K; ++j) F::template mac<SDWA>(F::kb(0), j * F::kTableBytes, cur[j], s);
-  }
-  F::pin(s);
-  const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
-  const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x;
-#pragma unroll
-  for (int q = 0; q < NR; ++q)
-    buf_st<(POL & kPolStoresCached) != 0>(par, lane_id() * 16, soff + q * p.frag_stride, F::row(s, q));
+  x = (w - o * p.tiles) * kTile + wave_in_block() * kChunkBytes;
 }
 
 // Edge item: payload tail and chunks reaching the zero padding past obj_len
@@ -479,8 +502,7 @@ __device__ __forceinline__ void encode_item(const EncodeParams& p, uint32_t w, u
 template <class F, int K, int NR>
 __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t e) {
   const uint32_t o = e / p.edge_tiles;
-  const uint32_t t = (p.tiles + (e - o * p.edge_tiles)) * (kWavesPerBlock * kChunkBytes) +
-                     threadIdx.x * 16;
+  const uint32_t t = (p.tiles + (e - o * p.edge_tiles)) * kTile + threadIdx.x * 16;
   if (t >= p.bs) return;
   const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride;
   const int64_t rem = static_cast<int64_t>(p.bs) - t;
@@ -498,102 +520,90 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
   for (int q = 0; q < NR; ++q) store_partial(par + q * p.frag_stride, F::row(s, q), rem);
 }
 
-// SDWA = false: the table addresses are built with v_perm (decode's form;
-// A/B of the benchmark case, ECAMD_ENC_PERM=1).
-template <class F, int K, int NR, int POL, bool SDWA = true, bool NOCOMP = false>
-__global__ void __launch_bounds__(kThreadsPerBlock) encode_kernel(EncodeParams p) {
+// Interior encode: object slices streamed in (default cache policy --
+// neighbouring slices share 128-B lines, which L2 then serves twice), parity
+// chunks stored nontemporal and line-aligned.  NOCOMP: memory-only probe
+// (inputs XORed, no lookups; wrong parity) for the benchmark shape.
+template <class F, int K, int NR, bool NOCOMP = false>
+__global__ void __launch_bounds__(kThreadsPerBlock)
+    __attribute__((amdgpu_waves_per_eu(kEncodeOcc, 8))) encode_kernel(EncodeParams p) {
+  constexpr int NB = stream_bufs<K>();
   load_tables(p.tables, K * F::kTableBytes, 0);
-  if (p.headers != nullptr && p.row0 == 0)
-    for (uint32_t o = blockIdx.x; o < p.n_obj; o += gridDim.x) {
-      const uint64_t base = static_cast<uint64_t>(o) * p.stripe_stride;
-      block_headers(p.parity + base, p.frag_stride, p.headers + K * kHeaderBytes, p.m);
-      if (p.data != nullptr) block_headers(p.data + base, p.frag_stride, p.headers, K);
-    }
   __syncthreads();
-  // edge items first, on the highest-numbered blocks (those with the fewest
-  // interior items)
-  const uint32_t n_edge = p.n_obj * p.edge_tiles;
-  for (uint32_t e = gridDim.x - 1 - blockIdx.x; e < n_edge; e += gridDim.x)
-    encode_edge_item<F, K, NR>(p, e);
-  const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
-  uint32_t w = r.begin;
-  if (w < r.end) {
-    uint4 xa[K], xb[K];
-    uint32_t o, x;
-    enc_item_pos(p, w, o, x);
-    encode_load<K, POL>(p, o, x, xa);
-    // two items per trip so cur / nxt stay compile-time register arrays
-    while (true) {
-      uint32_t wn = w + r.step < r.end ? w + r.step : w;
-      encode_item<F, K, NR, POL, SDWA, NOCOMP>(p, w, wn, xa, xb, wn == w);
-      if (wn == w) break;
-      w = wn;
-      wn = w + r.step < r.end ? w + r.step : w;
-      encode_item<F, K, NR, POL, SDWA, NOCOMP>(p, w, wn, xb, xa, wn == w);
-      if (wn == w) break;
-      w = wn;
-    }
-  }
-}
-
-// Prefetch depth 2 (A/B of the benchmark case, ECAMD_ENC_DEPTH2=1): while
-// item w is computed, items w + step and w + 2*step are in flight (three
-// register buffers; 3 waves per SIMD).
-template <class F, int K, int NR, int POL>
-__global__ void __launch_bounds__(kThreadsPerBlock) __attribute__((amdgpu_waves_per_eu(3, 8)))
-encode_kernel_d2(EncodeParams p) {
-  load_tables(p.tables, K * F::kTableBytes, 0);
-  if (p.headers != nullptr && p.row0 == 0)
-    for (uint32_t o = blockIdx.x; o < p.n_obj; o += gridDim.x) {
-      const uint64_t base = static_cast<uint64_t>(o) * p.stripe_stride;
-      block_headers(p.parity + base, p.frag_stride, p.headers + K * kHeaderBytes, p.m);
-      if (p.data != nullptr) block_headers(p.data + base, p.frag_stride, p.headers, K);
-    }
-  __syncthreads();
-  const uint32_t n_edge = p.n_obj * p.edge_tiles;
-  for (uint32_t e = gridDim.x - 1 - blockIdx.x; e < n_edge; e += gridDim.x)
-    encode_edge_item<F, K, NR>(p, e);
   const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
   uint32_t w = r.begin;
   if (w >= r.end) return;
-  uint4 xa[K], xb[K], xc[K];
-  // item w + k*step if it exists, else w itself (loaded through a
-  // zero-record descriptor: no traffic)
-  auto ahead = [&](uint32_t v, uint32_t k) { return v + k * r.step < r.end ? v + k * r.step : v; };
-  {
-    uint32_t o, x;
-    enc_item_pos(p, w, o, x);
-    encode_load<K, POL>(p, o, x, xa);
-    const uint32_t w1 = ahead(w, 1);
-    enc_item_pos(p, w1, o, x);
-    encode_load<K, POL>(p, o, x, xb, w1 == w);
-  }
+  uint32_t o, x;
+  enc_item_pos(p, w, o, x);
+  Rsrc cur = rsrc(p.objs + static_cast<uint64_t>(o) * p.obj_stride);
+  const uint32_t lane16 = lane_id() * 16;
+  uint4 buf[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) buf[j] = buf_ld<true>(cur, lane16, j * p.bs + x);
   while (true) {
-    uint32_t f = ahead(w, 2);
-    encode_item<F, K, NR, POL, true>(p, w, f, xa, xc, f == w);
-    if (w + r.step >= r.end) break;
-    w += r.step;
-    f = ahead(w, 2);
-    encode_item<F, K, NR, POL, true>(p, w, f, xb, xa, f == w);
-    if (w + r.step >= r.end) break;
-    w += r.step;
-    f = ahead(w, 2);
-    encode_item<F, K, NR, POL, true>(p, w, f, xc, xb, f == w);
-    if (w + r.step >= r.end) break;
-    w += r.step;
+    // the next item, or this one again through a zero-record descriptor
+    const uint32_t wn = w + r.step < r.end ? w + r.step : w;
+    uint32_t on, xn;
+    enc_item_pos(p, wn, on, xn);
+    const Rsrc nxt = rsrc(p.objs + static_cast<uint64_t>(on) * p.obj_stride, wn == w ? 0 : -1);
+    typename F::Acc s;
+    F::zero(s);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if constexpr (NOCOMP) {
+        uint32_t* a = reinterpret_cast<uint32_t*>(&s);
+        a[0] ^= buf[j % NB].x;
+        a[2] ^= buf[j % NB].y;
+        a[4] ^= buf[j % NB].z;
+        a[6] ^= buf[j % NB].w;
+      } else {
+        F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[j % NB], s);
+      }
+      if (j + NB < K)
+        buf[j % NB] = buf_ld<true>(cur, lane16, (j + NB) * p.bs + x);
+      else
+        buf[j % NB] = buf_ld<true>(nxt, lane16, (j + NB - K) * p.bs + xn);
+    }
+    F::pin(s);
+    const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
+    const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) buf_st(par, lane16, soff + q * p.frag_stride, F::row(s, q));
+    if (wn == w) break;
+    w = wn;
+    o = on;
+    x = xn;
+    cur = nxt;
   }
+}
+
+// Headers and edge items of an encode: a launch of their own, so their
+// registers (all K edge inputs at once) do not bound the interior loop's
+// occupancy.
+template <class F, int K, int NR>
+__global__ void __launch_bounds__(kThreadsPerBlock) encode_edge_kernel(EncodeParams p) {
+  load_tables(p.tables, K * F::kTableBytes, 0);
+  if (p.headers != nullptr && p.row0 == 0)
+    for (uint32_t o = blockIdx.x; o < p.n_obj; o += gridDim.x) {
+      const uint64_t base = static_cast<uint64_t>(o) * p.stripe_stride;
+      block_headers(p.parity + base, p.frag_stride, p.headers + K * kHeaderBytes, p.m);
+      if (p.data != nullptr) block_headers(p.data + base, p.frag_stride, p.headers, K);
+    }
+  __syncthreads();
+  for (uint32_t e = blockIdx.x; e < p.n_obj * p.edge_tiles; e += gridDim.x)
+    encode_edge_item<F, K, NR>(p, e);
 }
 
 // Data fragments (optional output of encode): the k padded object slices
 // copied into their fragment payloads.  Item = (object, fragment, 4 KiB).
 __global__ void __launch_bounds__(kThreadsPerBlock) copy_data_kernel(EncodeParams p) {
-  const uint32_t per_frag = (p.bs + kWavesPerBlock * kChunkBytes - 1) / (kWavesPerBlock * kChunkBytes);
+  const uint32_t per_frag = (p.bs + kTile - 1) / kTile;
   const uint32_t per_obj = p.k * per_frag;
   const uint32_t items = p.n_obj * per_obj;
   for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
     const uint32_t o = w / per_obj, rest = w - o * per_obj;
     const uint32_t j = rest / per_frag, c = rest - j * per_frag;
-    const uint32_t t = c * (kWavesPerBlock * kChunkBytes) + threadIdx.x * 16;
+    const uint32_t t = c * kTile + threadIdx.x * 16;
     if (t >= p.bs) continue;
     const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride;
     const uint4 x = load_clamped(obj, static_cast<uint64_t>(j) * p.bs + t, p.obj_len);
@@ -614,21 +624,13 @@ __global__ void __launch_bounds__(kThreadsPerBlock) copy_data_kernel(EncodeParam
 // the next item's set into registers together with its payload loads, so a
 // change costs a few ds_writes and one barrier, not an L2 round trip.
 //
-// Realigned object stores.  Decode writes data slice j of an object at
-// j*bs + t, and bs is rarely a multiple of 16 (419,432 = 8 mod 16 at 4 MiB,
-// k = 10), so a plain 16-B lane store would straddle two 16-B units (the
-// memory pipeline splits it in two, and the lines at both ends of every wave
-// access are written as partial lines: 448 us vs 378 us for the same stream
-// line-aligned, round 1).  The shift s = (j*bs) mod 16 is uniform over the
-// slice.  Decode chunks therefore advance 63 lanes (1008 B) and lane 0 holds
-// the previous chunk's last 16 B; lane L >= 1 stores the aligned unit that
-// starts s bytes below its own position -- the last s bytes of lane L-1
-// (DPP wave_shr:1) and its own first 16 - s bytes -- and lane 0's store is
-// dropped by the buffer range check (its voffset is past the descriptor's
-// 2 GiB of records), so every slice costs exactly one aligned dwordx4 store
-// instruction per chunk, with no carried state and no branch around it.  A
-// chunk at x covers slice bytes [x + 16 - s, x + 1024 - s); the head
-// [0, 16 - s) and the tail are edge items.
+// Object stores.  Decode writes data slice j of an object at j*bs + t, and
+// bs is rarely a multiple of 16 (419,432 = 8 mod 16 at 4 MiB, k = 10), so
+// lane stores straddle 16-B units.  Realigning them was measured three ways
+// and each lost to the plain stores (round 1-2, profiles/): an overlap lane
+// per chunk (1008-B chunks: +12 % HBM traffic), LDS-staged whole tiles (438
+// vs 444 us, and 3 waves per SIMD), and DPP-shifted units with half-unit
+// stores at the chunk ends (440.8 vs 436.6 us with the streaming kernel).
 
 struct Slots {
   uint32_t table;  // set in the current slot (0xFFFFFFFF = none)
@@ -640,26 +642,25 @@ struct TablePre {
   static constexpr int kChunks = K * F::kTableBytes / 16;
   static constexpr int kPer = (kChunks + kThreadsPerBlock - 1) / kThreadsPerBlock;
   uint4 v[kPer];
-  uint32_t table;
+  uint32_t table;  // set held in v (0xFFFFFFFF = none)
 };
 
+// Prefetch a table set into registers: always issued (exact wait counts),
+// through a zero-record descriptor -- zeros, no traffic -- when not needed;
+// lanes past the set's end are dropped by the range check.
 template <class F, int K>
-__device__ __forceinline__ void table_prefetch(const DecodeParams& p, uint32_t table,
+__device__ __forceinline__ void table_prefetch(const DecodeParams& p, uint32_t table, bool need,
                                                TablePre<F, K>& pre) {
-  const uint4* src = reinterpret_cast<const uint4*>(
-      p.tables + static_cast<uint64_t>(table) * (K * F::kTableBytes / 4));
+  constexpr uint32_t kBytes = K * F::kTableBytes;
+  const Rsrc t = rsrc(p.tables + static_cast<uint64_t>(table) * (kBytes / 4), need ? kBytes : 0);
 #pragma unroll
-  for (int i = 0; i < TablePre<F, K>::kPer; ++i) {
-    const uint32_t c = threadIdx.x + i * kThreadsPerBlock;
-    if (c < static_cast<uint32_t>(TablePre<F, K>::kChunks)) pre.v[i] = src[c];
-  }
-  pre.table = table;
+  for (int i = 0; i < TablePre<F, K>::kPer; ++i)
+    pre.v[i] = buf_ld<true>(t, (threadIdx.x + i * kThreadsPerBlock) * 16, 0);
+  pre.table = need ? table : 0xFFFFFFFFu;
 }
 
-// Make d's table set current; returns its kb.  Block-uniform (barrier;
-// SYNC: a barrier even when the set is unchanged -- the staged stores'
-// write-after-read fence on the staging area).
-template <class F, int K, bool SYNC = false, class D>
+// Make d's table set current; returns its kb.  Block-uniform (barrier).
+template <class F, int K, class D>
 __device__ __forceinline__ uint32_t ensure_tables(const DecodeParams& p, const D& d, Slots& st,
                                                   const TablePre<F, K>& pre) {
   constexpr uint32_t kSlot = table_slot_bytes(K, F::kW);
@@ -686,28 +687,15 @@ __device__ __forceinline__ uint32_t ensure_tables(const DecodeParams& p, const D
     }
     __syncthreads();
     st.table = d.table();
-  } else if constexpr (SYNC) {
-    __syncthreads();
   }
   return F::kb(st.slot * kSlot);
 }
 
 enum DecodeMode : int {
-  kDecode = 0,        // one pass holds every missing row: all k data slices stored
+  kDecode = 0,        // one pass holds every missing row
   kReconstruct = 1,   // one fragment per object (aligned payload)
   kDecodeGeneric = 2  // more than 4 missing data fragments (several passes)
 };
-
-// Chunk stride: decode overlaps one lane (realigned slices) unless PLAIN
-// (lane stores at their natural, unaligned positions -- kept for A/B).
-template <int MODE, bool PLAIN>
-__host__ __device__ constexpr bool overlaps() {
-  return MODE != kReconstruct && !PLAIN;
-}
-template <int MODE, bool PLAIN>
-__host__ __device__ constexpr uint32_t chunk_stride() {
-  return overlaps<MODE, PLAIN>() ? kChunkBytes - 16 : kChunkBytes;
-}
 
 // An object's descriptor held in SGPRs.  The descriptor array is read with
 // vector loads (hipcc cannot prove the kernel's stores leave it untouched, so
@@ -748,22 +736,10 @@ __device__ __forceinline__ uint32_t in_pos(const DecodeParams& p, const DescU& d
   return p.compact ? static_cast<uint32_t>(c) : d.in_idx(c);
 }
 
-template <int MODE, bool PLAIN>
 __device__ __forceinline__ void dec_item_pos(const DecodeParams& p, uint32_t w, uint32_t& o,
                                              uint32_t& x) {
-  constexpr uint32_t kStride = chunk_stride<MODE, PLAIN>();
   o = w / p.tiles;
-  x = (w - o * p.tiles) * (kWavesPerBlock * kStride) + wave_in_block() * kStride;
-}
-
-template <int K, int POL>
-__device__ __forceinline__ void decode_load(const DecodeParams& p, uint32_t o, const DescU& d,
-                                            uint32_t x, uint4 (&v)[K], bool none = false) {
-  const Rsrc in = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride, none ? 0 : -1);
-#pragma unroll
-  for (int j = 0; j < K; ++j)
-    v[j] = buf_ld<(POL & kPolLoadsCached) != 0>(
-        in, lane_id() * 16, in_pos(p, d, j) * p.frag_stride + kHeaderBytes + x);
+  x = (w - o * p.tiles) * kTile + wave_in_block() * kChunkBytes;
 }
 
 // Output descriptor: 2 GiB - 1 records, so a voffset of kDrop (2 GiB) makes
@@ -777,254 +753,94 @@ __device__ __forceinline__ Rsrc rsrc_out(const void* base) {
       reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, 0x7FFFFFFF, 0x00020000);
 }
 
-__device__ __forceinline__ uint32_t shr1(uint32_t v) {
-  return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(
-      0, static_cast<int>(v), 0x138 /* wave_shr:1 */, 0xF, 0xF, false));
-}
-
-// Store slice unit: this lane's 16 B v sits at slice position x + 16*lane,
-// object offset soff + 16*lane with soff mod 16 == s; lane L >= 1 writes the
-// aligned unit at soff + 16*L - s, lane 0 is dropped (vst = kDrop).  Only
-// the dwords of lane L-1 that the unit uses are moved (d = (16 - s) / 4).
-// Every path issues exactly one store instruction.
-template <bool CACHED>
-__device__ __forceinline__ void st_unit(Rsrc out, uint32_t vst, uint32_t soff, const uint4& v,
-                                        uint32_t s) {
-  if (s == 0) {
-    buf_st<CACHED>(out, vst, soff, v);
-    return;
-  }
-  const uint32_t r = (16u - s) & 3u;
-  uint4 u;
-  switch ((16u - s) >> 2) {
-    case 0: {
-      const uint32_t p0 = shr1(v.x), p1 = shr1(v.y), p2 = shr1(v.z), p3 = shr1(v.w);
-      u = make_uint4(__builtin_amdgcn_alignbyte(p1, p0, r), __builtin_amdgcn_alignbyte(p2, p1, r),
-                     __builtin_amdgcn_alignbyte(p3, p2, r), __builtin_amdgcn_alignbyte(v.x, p3, r));
-      break;
-    }
-    case 1: {
-      const uint32_t p1 = shr1(v.y), p2 = shr1(v.z), p3 = shr1(v.w);
-      u = make_uint4(__builtin_amdgcn_alignbyte(p2, p1, r), __builtin_amdgcn_alignbyte(p3, p2, r),
-                     __builtin_amdgcn_alignbyte(v.x, p3, r), __builtin_amdgcn_alignbyte(v.y, v.x, r));
-      break;
-    }
-    case 2: {
-      const uint32_t p2 = shr1(v.z), p3 = shr1(v.w);
-      u = make_uint4(__builtin_amdgcn_alignbyte(p3, p2, r), __builtin_amdgcn_alignbyte(v.x, p3, r),
-                     __builtin_amdgcn_alignbyte(v.y, v.x, r), __builtin_amdgcn_alignbyte(v.z, v.y, r));
-      break;
-    }
-    default: {
-      const uint32_t p3 = shr1(v.w);
-      u = make_uint4(__builtin_amdgcn_alignbyte(v.x, p3, r), __builtin_amdgcn_alignbyte(v.y, v.x, r),
-                     __builtin_amdgcn_alignbyte(v.z, v.y, r), __builtin_amdgcn_alignbyte(v.w, v.z, r));
-      break;
-    }
-  }
-  buf_st<CACHED>(out, vst, soff - s, u);
-}
-
-// Staged object stores (STAGED, kDecode).  The block's four waves hold the
-// 4 KiB tile [t0, t0 + 4096) of every slice; they write it to LDS (slice c
-// at stage + c * 4096), and after a barrier thread u stores the 16-B-aligned
-// object unit u of each slice: slice j's tile lands at A = j*bs + t0, so with
-// a = A mod 16 unit u covers tile bytes [16u - a, 16u - a + 16) -- the last
-// a bytes of staged unit u - 1 and the first 16 - a of unit u (two aligned
-// ds_read_b128 and a funnel shift).  Every store is a whole aligned 16-B
-// unit except the two at the tile's ends (unit 0: bytes [a, 16); unit 256:
-// bytes [0, a)), so a slice's lines are split only where two tiles meet
-// (every 4 KiB), not at every wave's 1 KiB as with lane-natural stores.
-constexpr uint32_t kStageTile = kWavesPerBlock * kChunkBytes;  // 4096
-
-// Bytes [lo, hi) of v stored at voff + lo (naturally aligned pieces).
-__device__ __forceinline__ void buf_st_bytes(Rsrc r, uint32_t voff, const uint4& v, uint32_t lo,
-                                             uint32_t hi) {
-  const uint64_t q0 = v.x | (static_cast<uint64_t>(v.y) << 32);
-  const uint64_t q1 = v.z | (static_cast<uint64_t>(v.w) << 32);
-  for (uint32_t i = lo; i < hi;) {
-    const uint64_t qv = i < 8 ? q0 >> (8 * i) : q1 >> (8 * (i - 8));
-    if ((i & 7) == 0 && i + 8 <= hi) {
-      v2u d;
-      d.x = static_cast<uint32_t>(qv);
-      d.y = static_cast<uint32_t>(qv >> 32);
-      __builtin_amdgcn_raw_buffer_store_b64(d, r, voff + i, 0, 0);
-      i += 8;
-    } else if ((i & 3) == 0 && i + 4 <= hi) {
-      __builtin_amdgcn_raw_buffer_store_b32(static_cast<uint32_t>(qv), r, voff + i, 0, 0);
-      i += 4;
-    } else if ((i & 1) == 0 && i + 2 <= hi) {
-      __builtin_amdgcn_raw_buffer_store_b16(static_cast<unsigned short>(qv), r, voff + i, 0, 0);
-      i += 2;
-    } else {
-      __builtin_amdgcn_raw_buffer_store_b8(static_cast<unsigned char>(qv), r, voff + i, 0, 0);
-      i += 1;
-    }
-  }
-}
-
-// Bytes [b0, b0 + 16) of the 32-byte pair (lo, hi), b0 = 16 - a in 1..15
-// (wave-uniform).
-__device__ __forceinline__ uint4 funnel16(const uint4& lo, const uint4& hi, uint32_t b0) {
-  const uint32_t r = b0 & 3u;
-  switch (b0 >> 2) {
-    case 0:
-      return make_uint4(__builtin_amdgcn_alignbyte(lo.y, lo.x, r), __builtin_amdgcn_alignbyte(lo.z, lo.y, r),
-                        __builtin_amdgcn_alignbyte(lo.w, lo.z, r), __builtin_amdgcn_alignbyte(hi.x, lo.w, r));
-    case 1:
-      return make_uint4(__builtin_amdgcn_alignbyte(lo.z, lo.y, r), __builtin_amdgcn_alignbyte(lo.w, lo.z, r),
-                        __builtin_amdgcn_alignbyte(hi.x, lo.w, r), __builtin_amdgcn_alignbyte(hi.y, hi.x, r));
-    case 2:
-      return make_uint4(__builtin_amdgcn_alignbyte(lo.w, lo.z, r), __builtin_amdgcn_alignbyte(hi.x, lo.w, r),
-                        __builtin_amdgcn_alignbyte(hi.y, hi.x, r), __builtin_amdgcn_alignbyte(hi.z, hi.y, r));
-    default:
-      return make_uint4(__builtin_amdgcn_alignbyte(hi.x, lo.w, r), __builtin_amdgcn_alignbyte(hi.y, hi.x, r),
-                        __builtin_amdgcn_alignbyte(hi.z, hi.y, r), __builtin_amdgcn_alignbyte(hi.w, hi.z, r));
-  }
-}
-
-// Store one staged slice tile (LDS bytes [sb, sb + 4096), preceded by 16
-// readable bytes) at object offset A.  Block-wide; after the staging barrier.
-template <bool CACHED>
-__device__ __forceinline__ void stage_out(Rsrc out, uint32_t sb, uint32_t A) {
-  const uint32_t u = threadIdx.x;
-  const uint32_t a = A & 15u, U0 = A - a;
-  const v4u c = *lds_v4(sb + 16 * u);
-  const uint4 cu = make_uint4(c.x, c.y, c.z, c.w);
-  if (a == 0) {
-    buf_st<CACHED>(out, 16 * u, U0, cu);
-    return;
-  }
-  const v4u p = *lds_v4(sb + 16 * u - 16);
-  const uint4 v = funnel16(make_uint4(p.x, p.y, p.z, p.w), cu, 16 - a);
-  if (u != 0)
-    buf_st<CACHED>(out, 16 * u, U0, v);
-  else
-    buf_st_bytes(out, U0, v, a, 16);
-  if (u == kThreadsPerBlock - 1) {
-    // unit 256: the last a bytes of staged unit 255
-    const uint4 t = funnel16(cu, make_uint4(0, 0, 0, 0), 16 - a);
-    buf_st_bytes(out, U0 + 16 * kThreadsPerBlock, t, 0, a);
-  }
-}
-
-// kDecode: the k inputs are the first k available fragments in ascending
-// order, so the present data fragments come first and the parity inputs --
-// as many as there are missing data slices, e -- are the last e.  After the
-// products, row q overwrites parity input K-e+q: cur[c] then holds data slice
-// slice_of(c) for every c, and all K slices are stored unconditionally.
-__device__ __forceinline__ uint32_t slice_of(const DescU& d, uint32_t e, int K, int c) {
-  return c < K - static_cast<int>(e) ? d.in_idx(c) : d.out_idx(c - (K - static_cast<int>(e)));
-}
-
-template <class F, int K>
-__device__ __forceinline__ void place_rows(const typename F::Acc& s, uint32_t e, uint4 (&x)[K]) {
-  constexpr int L = K < 4 ? K : 4;
-  switch (e) {
-#define ECAMD_PLACE(E)                                                                     \
-  case E:                                                                                  \
-    if constexpr (E <= L) {                                                                \
-      _Pragma("unroll") for (int q = 0; q < E; ++q) x[K - E + q] = F::row(s, q);           \
-    }                                                                                      \
-    break;
-    ECAMD_PLACE(1) ECAMD_PLACE(2) ECAMD_PLACE(3) ECAMD_PLACE(4)
-#undef ECAMD_PLACE
-    default:
-      break;
-  }
-}
-
-// One interior decode / reconstruct item with inputs in `cur`; prefetches the
-// block's next item (payloads into `nxt`, its table set into `pre`).
-template <class F, int K, int MODE, bool PLAIN, int POL, bool STAGED, bool NOCOMP = false>
-__device__ __forceinline__ void decode_item(const DecodeParams& p, uint32_t w, uint32_t wn,
-                                            Slots& st, TablePre<F, K>& pre, uint4 (&cur)[K],
-                                            uint4 (&nxt)[K]) {
-  uint32_t o, x, on, xn;
-  dec_item_pos<MODE, PLAIN>(p, w, o, x);
-  dec_item_pos<MODE, PLAIN>(p, wn, on, xn);
-  const DescU dn = load_desc(p, on);
-  decode_load<K, POL>(p, on, dn, xn, nxt, wn == w);
-  const DescU d = load_desc(p, o);
-  const uint32_t kb = ensure_tables<F, K, STAGED>(p, d, st, pre);
-  if (dn.n_out() != 0 && dn.table() != st.table && dn.table() != pre.table)
-    table_prefetch<F, K>(p, dn.table(), pre);
-  const uint32_t n_out = d.n_out();
-  typename F::Acc s;
-  F::zero(s);
-  if (!NOCOMP && n_out != 0) {
+// Interior decode / reconstruct, streaming the first k available fragments.
+//   decode (and each pass of a multi-pass decode): a present data input --
+//   descriptor copy_inputs set and input index < k -- is stored to its object
+//   slice as soon as its products are taken (before its registers are
+//   refilled); the n_out rebuilt rows after the last input.
+//   reconstruct: row 0 into the fragment payload.
+// Stores that do not apply (parity inputs, rows past n_out) go to voffset
+// kDrop and are discarded by the range check, so every item issues the same
+// memory instructions.  NOCOMP: memory-only probe (no lookups; wrong rows).
+template <class F, int K, int MODE, bool NOCOMP = false>
+__global__ void __launch_bounds__(kThreadsPerBlock)
+    __attribute__((amdgpu_waves_per_eu(kDecodeOcc, 8))) decode_kernel(DecodeParams p) {
+  constexpr int NB = stream_bufs<K>();
+  Slots st{0xFFFFFFFFu, 1u};
+  TablePre<F, K> pre;
+  const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
+  uint32_t w = r.begin;
+  if (w >= r.end) return;  // block-uniform: no wave of this block reaches a barrier
+  const uint32_t lane16 = lane_id() * 16;
+  uint32_t o, x;
+  dec_item_pos(p, w, o, x);
+  DescU d = load_desc(p, o);
+  Rsrc cur = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride);
+  uint4 buf[NB];
 #pragma unroll
-    for (int j = 0; j < K; ++j) F::mac(kb, j * F::kTableBytes, cur[j], s);
-  }
-  F::pin(s);
-  constexpr bool kStC = (POL & kPolStoresCached) != 0;
-  uint8_t* const outp = p.out + static_cast<uint64_t>(o) * p.out_stride;
-  if constexpr (MODE == kReconstruct) {
-    buf_st<kStC>(rsrc(outp), lane_id() * 16, kHeaderBytes + x, F::row(s, 0));
-  } else {
-    // overlap: lane 0 only carries the previous chunk's bytes, its store is
-    // dropped; plain: every lane stores its own 16 B where they belong
-    const Rsrc out = PLAIN ? rsrc(outp) : rsrc_out(outp);
-    const uint32_t vst = (!PLAIN && lane_id() == 0) ? kDrop : lane_id() * 16;
-    auto put = [&](uint32_t off, const uint4& v) {
-      if constexpr (PLAIN)
-        buf_st<kStC>(out, vst, off + x, v);
+  for (int j = 0; j < NB; ++j)
+    buf[j] = buf_ld(cur, lane16, in_pos(p, d, j) * p.frag_stride + kHeaderBytes + x);
+  table_prefetch<F, K>(p, d.table(), d.n_out() != 0, pre);
+  while (true) {
+    const uint32_t wn = w + r.step < r.end ? w + r.step : w;
+    uint32_t on, xn;
+    dec_item_pos(p, wn, on, xn);
+    const DescU dn = load_desc(p, on);
+    const Rsrc nxt = rsrc(p.frags + static_cast<uint64_t>(on) * p.stripe_stride, wn == w ? 0 : -1);
+    const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
+    table_prefetch<F, K>(p, dn.table(), wn != w && dn.n_out() != 0 && dn.table() != st.table,
+                         pre);
+    const Rsrc out = rsrc_out(p.out + static_cast<uint64_t>(o) * p.out_stride);
+    const bool copy = MODE != kReconstruct && d.copy_inputs() != 0;
+    typename F::Acc s;
+    F::zero(s);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if constexpr (NOCOMP) {
+        uint32_t* a = reinterpret_cast<uint32_t*>(&s);
+        a[0] ^= buf[j % NB].x;
+      } else {
+        F::mac(kb, j * F::kTableBytes, buf[j % NB], s);
+      }
+      if constexpr (MODE != kReconstruct)
+        buf_st(out, copy && d.in_idx(j) < static_cast<uint32_t>(K) ? lane16 : kDrop,
+               d.in_idx(j) * p.bs + x, buf[j % NB]);
+      if (j + NB < K)
+        buf[j % NB] = buf_ld(cur, lane16, in_pos(p, d, j + NB) * p.frag_stride + kHeaderBytes + x);
       else
-        st_unit<kStC>(out, vst, off + x, v, off & 15u);
-    };
-    if constexpr (MODE == kDecode && STAGED) {
-      place_rows<F, K>(s, n_out, cur);
-      constexpr uint32_t sb0 = 2 * table_slot_bytes(K, F::kW) + 16;
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        v4u v;
-        v.x = cur[j].x;
-        v.y = cur[j].y;
-        v.z = cur[j].z;
-        v.w = cur[j].w;
-        *lds_v4(sb0 + j * kStageTile + wave_in_block() * kChunkBytes + lane_id() * 16) = v;
-      }
-      __syncthreads();
-      const uint32_t t0 = x - wave_in_block() * kChunkBytes;
-      const Rsrc outb = rsrc(outp);
-#pragma unroll
-      for (int j = 0; j < K; ++j)
-        stage_out<kStC>(outb, sb0 + j * kStageTile, slice_of(d, n_out, K, j) * p.bs + t0);
-    } else if constexpr (MODE == kDecode) {
-      place_rows<F, K>(s, n_out, cur);
-#pragma unroll
-      for (int j = 0; j < K; ++j) put(slice_of(d, n_out, K, j) * p.bs, cur[j]);
-    } else {
-      if (d.copy_inputs()) {
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          const uint32_t idx = d.in_idx(j);
-          if (idx < static_cast<uint32_t>(K)) put(idx * p.bs, cur[j]);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < kRowsPerPass; ++q)
-        if (q < static_cast<int>(n_out)) put(d.out_idx(q) * p.bs, F::row(s, q));
+        buf[j % NB] =
+            buf_ld(nxt, lane16, in_pos(p, dn, j + NB - K) * p.frag_stride + kHeaderBytes + xn);
     }
+    F::pin(s);
+    if constexpr (MODE == kReconstruct) {
+      buf_st(out, lane16, kHeaderBytes + x, F::row(s, 0));
+    } else {
+      const uint32_t e = d.n_out();
+#pragma unroll
+      for (int q = 0; q < F::kRows; ++q)
+        buf_st(out, q < static_cast<int>(e) ? lane16 : kDrop, d.out_idx(q) * p.bs + x,
+               F::row(s, q));
+    }
+    if (wn == w) break;
+    w = wn;
+    o = on;
+    x = xn;
+    d = dn;
+    cur = nxt;
   }
 }
 
-// Edge item: 4 KiB of positions from q0 (+ 16 per thread), byte-exact stores
-// clipped to each output's window.  Decode: head item (window [0, 16 - s))
-// and tail items (window [tiles*4032 + 16 - s, object bytes of the slice)).
-// Reconstruct: tail items [tiles*4096, bs).
-template <class F, int K, int MODE, bool PLAIN>
+// Edge item: 4 KiB of positions from the end of the interior tiles (+ 16 per
+// thread), byte-exact stores clipped to each output's window: an object
+// slice's bytes inside the object (decode), or the payload (reconstruct).
+template <class F, int K, int MODE>
 __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t e, Slots& st,
                                                  const TablePre<F, K>& pre) {
-  constexpr bool kOv = overlaps<MODE, PLAIN>();
   const uint32_t o = e / p.edge_tiles;
-  const uint32_t ei = e - o * p.edge_tiles;
-  const uint32_t tail0 = p.tiles * kWavesPerBlock * chunk_stride<MODE, PLAIN>();
-  const bool head = kOv && ei == 0;
-  const uint32_t q0 = head ? 0u : tail0 + (ei - (kOv ? 1u : 0u)) * 4096u;
+  const uint32_t tail0 = p.tiles * kTile;
   const DescU d = load_desc(p, o);
   const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
-  const uint32_t t = q0 + threadIdx.x * 16;
+  const uint32_t t = tail0 + (e - o * p.edge_tiles) * kTile + threadIdx.x * 16;
   if (t >= p.bs) return;
   uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
   // t < bs and 16 | t, so t + 16 <= round16(bs) <= frag_stride - 80: in bounds
@@ -1044,39 +860,26 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
     if (d.n_out() != 0) store_window(out + kHeaderBytes, t, F::row(s, 0), tail0, p.bs);
     return;
   }
-  // window of slice j: [lo_j, hi_j) in slice positions
-  auto window = [&](uint32_t j, int64_t& lo, int64_t& hi) {
-    const uint32_t sh = (j * p.bs) & 15u;
-    const int64_t valid = object_bytes(j, p.bs, 0, p.obj_len);
-    lo = head ? 0 : static_cast<int64_t>(tail0) + (kOv ? 16 - sh : 0);
-    hi = head ? 16 - sh : valid;
-    if (hi > valid) hi = valid;
-  };
   if (d.copy_inputs()) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       const uint32_t idx = d.in_idx(j);
       if (idx >= K) continue;
-      int64_t lo, hi;
-      window(idx, lo, hi);
-      store_window(out + static_cast<uint64_t>(idx) * p.bs, t, x[j], lo, hi);
+      store_window(out + static_cast<uint64_t>(idx) * p.bs, t, x[j], tail0,
+                   object_bytes(idx, p.bs, 0, p.obj_len));
     }
   }
   for (uint32_t q = 0; q < d.n_out(); ++q) {
     const uint32_t idx = d.out_idx(q);
-    int64_t lo, hi;
-    window(idx, lo, hi);
-    store_window(out + static_cast<uint64_t>(idx) * p.bs, t, F::row(s, q), lo, hi);
+    store_window(out + static_cast<uint64_t>(idx) * p.bs, t, F::row(s, q), tail0,
+                 object_bytes(idx, p.bs, 0, p.obj_len));
   }
 }
 
-// OCC = minimum waves per SIMD the register allocation must allow (hipcc
-// left alone spends ~140 VGPRs on the decode variants: 3 waves per SIMD; 4
-// fits in 128 VGPRs with a few spills around the table prefetch).
-template <class F, int K, int MODE, int OCC, bool PLAIN, int POL, bool STAGED = false,
-          bool NOCOMP = false>
-__global__ void __launch_bounds__(kThreadsPerBlock) __attribute__((amdgpu_waves_per_eu(OCC, 8)))
-decode_kernel(DecodeParams p) {
+// Reconstruct headers and the edge items of a decode / reconstruct (own
+// launch, own registers).
+template <class F, int K, int MODE>
+__global__ void __launch_bounds__(kThreadsPerBlock) decode_edge_kernel(DecodeParams p) {
   if (MODE == kReconstruct && p.headers != nullptr)
     for (uint32_t o = blockIdx.x; o < p.n_obj; o += gridDim.x)
       block_headers(p.out + static_cast<uint64_t>(o) * p.out_stride, 0,
@@ -1084,30 +887,8 @@ decode_kernel(DecodeParams p) {
   Slots st{0xFFFFFFFFu, 1u};
   TablePre<F, K> pre;
   pre.table = 0xFFFFFFFFu;
-  // edge items first, on the highest-numbered blocks
-  const uint32_t n_edge = p.n_obj * p.edge_tiles;
-  for (uint32_t e = gridDim.x - 1 - blockIdx.x; e < n_edge; e += gridDim.x)
-    decode_edge_item<F, K, MODE, PLAIN>(p, e, st, pre);
-  const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
-  uint32_t w = r.begin;
-  if (w < r.end) {
-    uint4 xa[K], xb[K];
-    uint32_t o, x;
-    dec_item_pos<MODE, PLAIN>(p, w, o, x);
-    const DescU d0 = load_desc(p, o);
-    decode_load<K, POL>(p, o, d0, x, xa);
-    if (d0.n_out() != 0 && d0.table() != st.table) table_prefetch<F, K>(p, d0.table(), pre);
-    while (true) {
-      uint32_t wn = w + r.step < r.end ? w + r.step : w;
-      decode_item<F, K, MODE, PLAIN, POL, STAGED, NOCOMP>(p, w, wn, st, pre, xa, xb);
-      if (wn == w) break;
-      w = wn;
-      wn = w + r.step < r.end ? w + r.step : w;
-      decode_item<F, K, MODE, PLAIN, POL, STAGED, NOCOMP>(p, w, wn, st, pre, xb, xa);
-      if (wn == w) break;
-      w = wn;
-    }
-  }
+  for (uint32_t e = blockIdx.x; e < p.n_obj * p.edge_tiles; e += gridDim.x)
+    decode_edge_item<F, K, MODE>(p, e, st, pre);
 }
 
 // ---------------- launch ----------------
@@ -1118,21 +899,29 @@ inline bool env_flag(const char* name, bool dflt) {
   return v[0] != '0';
 }
 
-inline int grid_for(const void* kernel, size_t lds_bytes, uint32_t items) {
-  int dev = 0, cus = 256, per_cu = 4;
-  if (hipGetDevice(&dev) == hipSuccess) {
+// Blocks per CU that are resident at once: the occupancy API's answer capped
+// by the register file (512 VGPRs per lane per SIMD, one wave per SIMD per
+// block) -- the API can report one block per CU more than fits
+// (MI355X_MICROARCH.md, Residency), and a grid-stride kernel must not queue
+// blocks behind the resident ones -- and by `max_per_cu`.
+inline int resident_per_cu(const void* kernel, size_t lds_bytes, int max_per_cu) {
+  int per_cu = max_per_cu;
+  int b = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kThreadsPerBlock, lds_bytes) ==
+          hipSuccess &&
+      b > 0)
+    per_cu = std::min(per_cu, b);
+  hipFuncAttributes attr{};
+  if (hipFuncGetAttributes(&attr, kernel) == hipSuccess && attr.numRegs > 0)
+    per_cu = std::min(per_cu, 512 / ((attr.numRegs + 7) / 8 * 8));
+  return std::max(per_cu, 1);
+}
+
+inline int grid_for(const void* kernel, size_t lds_bytes, uint32_t items, int max_per_cu) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kThreadsPerBlock, lds_bytes) ==
-            hipSuccess &&
-        b > 0)
-      per_cu = b;
-  }
-  // The occupancy API can report one block per CU more than fits
-  // (MI355X_MICROARCH.md, Residency); a grid-stride kernel must not queue
-  // blocks behind the resident ones, so stay at <= 4 per CU.
-  per_cu = std::min(per_cu, 4);
-  const uint32_t resident = static_cast<uint32_t>(cus * per_cu);
+  const uint32_t resident = static_cast<uint32_t>(cus * resident_per_cu(kernel, lds_bytes, max_per_cu));
   return static_cast<int>(items < resident ? (items ? items : 1) : resident);
 }
 
@@ -1152,11 +941,12 @@ inline bool lds_starts_at_zero(const void* kern) {
 }
 
 template <typename Kern, typename Params>
-hipError_t launch(Kern kern, Params p, size_t lds, uint32_t items, hipStream_t stream) {
+hipError_t launch(Kern kern, Params p, size_t lds, uint32_t items, hipStream_t stream,
+                  int max_per_cu = 4) {
   if (items == 0) return hipSuccess;
   const void* k = reinterpret_cast<const void*>(kern);
   if (!lds_starts_at_zero(k)) return hipErrorInvalidKernelFile;
-  const int grid = grid_for(k, lds, items);
+  const int grid = grid_for(k, lds, items, max_per_cu);
   p.xcd_split = (grid >= 8 && grid % 8 == 0 && env_flag("ECAMD_XCD", true)) ? 1u : 0u;
 
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreadsPerBlock), lds, stream, p);
@@ -1171,59 +961,27 @@ inline int64_t last_room(uint32_t bs, uint64_t obj_len, uint32_t k) {
   return room < 0 ? 0 : room;
 }
 
-// Cache-policy variant requested through the environment (A/B of the
-// benchmark case only): ECAMD_LD_CACHED=0/1, ECAMD_ST_CACHED=0/1.
-inline int env_policy(int dflt) {
-  return (env_flag("ECAMD_LD_CACHED", dflt & kPolLoadsCached) ? kPolLoadsCached : 0) |
-         (env_flag("ECAMD_ST_CACHED", dflt & kPolStoresCached) ? kPolStoresCached : 0);
-}
-
-// Defaults, measured on MI355X (round 2, tools/ab_bench.py, k=10 m=4,
-// 256 x 4 MiB): encode reads the object slices with the default cache
-// policy -- neighbouring slices share 128-B lines, which L2 then serves
-// twice (303 vs 308 us); stores stay nontemporal (cached: 331 us).
-// Decode stores each lane's 16 B where they belong (446 us) rather than
-// through the overlap-lane realignment (456 us): the 1008-B chunks it needs
-// cost 12 % more HBM reads and writes than the aligned units save.
-constexpr int kEncodePolicy = kPolLoadsCached;
-constexpr bool kDecodePlain = true;
-constexpr bool kDecodeStaged = false;
-
+// Encode: headers + edge items, then the interior stream, then (optionally)
+// the data fragments.  Interior tiles: 4 KiB of positions ending at or before
+// min(bs, room).  ECAMD_ENC_NOCOMP=1: memory-only probe of the benchmark
+// shape (tools/ab_bench.py).
 template <class F, int K, int NR>
 hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
-  // interior tiles: 4 KiB of positions ending at or before min(bs, room)
-  const uint32_t tile = kWavesPerBlock * kChunkBytes;
-  p.tiles = static_cast<uint32_t>(last_room(p.bs, p.obj_len, K) / tile);
-  p.edge_tiles = (p.bs + tile - 1) / tile - p.tiles;
-  const uint32_t items = std::max(std::max(p.n_obj * p.tiles, p.n_obj * p.edge_tiles),
-                                  p.headers ? p.n_obj : 0u);
-  hipError_t e = hipErrorInvalidValue;
-  const int pol = (K == 10 && NR == 4) ? env_policy(kEncodePolicy) : kEncodePolicy;
-  bool sdwa = true;
-  if constexpr (K == 10 && NR == 4) sdwa = !env_flag("ECAMD_ENC_PERM", false);
-  if constexpr (K == 10 && NR == 4) {
-    if (pol == kEncodePolicy && env_flag("ECAMD_ENC_NOCOMP", false))
-      return launch(encode_kernel<F, K, NR, kEncodePolicy, true, true>, p, K * F::kTableBytes,
-                    items, stream);
-    if (pol == kEncodePolicy && env_flag("ECAMD_ENC_DEPTH2", false)) {
-      e = launch(encode_kernel_d2<F, K, NR, kEncodePolicy>, p, K * F::kTableBytes, items, stream);
-      if (e != hipSuccess || p.data == nullptr || p.row0 != 0) return e;
-      return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + tile - 1) / tile), stream);
-    }
-  }
-  if (pol == kEncodePolicy && !sdwa) {
-    if constexpr (K == 10 && NR == 4)
-      e = launch(encode_kernel<F, K, NR, kEncodePolicy, false>, p, K * F::kTableBytes, items, stream);
-  } else if (pol == kEncodePolicy)
-    e = launch(encode_kernel<F, K, NR, kEncodePolicy>, p, K * F::kTableBytes, items, stream);
-  else if constexpr (K == 10 && NR == 4)
-    e = pol == 0   ? launch(encode_kernel<F, K, NR, 0>, p, K * F::kTableBytes, items, stream)
-        : pol == 2 ? launch(encode_kernel<F, K, NR, 2>, p, K * F::kTableBytes, items, stream)
-                   : launch(encode_kernel<F, K, NR, 3>, p, K * F::kTableBytes, items, stream);
+  p.tiles = static_cast<uint32_t>(last_room(p.bs, p.obj_len, K) / kTile);
+  p.edge_tiles = (p.bs + kTile - 1) / kTile - p.tiles;
+  constexpr size_t lds = K * F::kTableBytes;
+  hipError_t e = launch(encode_edge_kernel<F, K, NR>, p, lds,
+                        std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u), stream);
+  if (e != hipSuccess) return e;
+  bool probe = false;
+  if constexpr (K == 10 && NR == 4) probe = env_flag("ECAMD_ENC_NOCOMP", false);
+  if constexpr (K == 10 && NR == 4)
+    e = probe ? launch(encode_kernel<F, K, NR, true>, p, lds, p.n_obj * p.tiles, stream, kEncodePerCu)
+              : launch(encode_kernel<F, K, NR>, p, lds, p.n_obj * p.tiles, stream, kEncodePerCu);
   else
-    e = hipErrorInvalidValue;
+    e = launch(encode_kernel<F, K, NR>, p, lds, p.n_obj * p.tiles, stream, kEncodePerCu);
   if (e != hipSuccess || p.data == nullptr || p.row0 != 0) return e;
-  return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + tile - 1) / tile), stream);
+  return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + kTile - 1) / kTile), stream);
 }
 
 template <class F, int K>
@@ -1242,80 +1000,36 @@ hipError_t launch_encode_rows(const EncodeParams& p, hipStream_t stream) {
   }
 }
 
-constexpr int kDecodeOcc = 4;
-
-// LDS of a decode launch: two table slots (+ the staging area).
-template <class F, int K, bool STAGED>
-constexpr uint32_t decode_lds_bytes() {
-  return 2 * table_slot_bytes(K, F::kW) + (STAGED ? 16 + K * kStageTile : 0);
-}
-// Staged stores need K * 4 KiB of LDS per block; used while two blocks per
-// CU still fit (k <= 16 for GF(2^16)).
+// LDS of a decode launch: two table slots.
 template <class F, int K>
-constexpr bool staged_fits() {
-  return decode_lds_bytes<F, K, true>() <= 80u * 1024u;
+constexpr uint32_t decode_lds_bytes() {
+  return 2 * table_slot_bytes(K, F::kW);
 }
 
-template <class F, int K, int MODE, int OCC, bool PLAIN, int POL = 0, bool STAGED = false,
-          bool NOCOMP = false>
-hipError_t launch_decode_variant(DecodeParams p, hipStream_t stream) {
-  constexpr uint32_t tile = kWavesPerBlock * chunk_stride<MODE, PLAIN>();
-  if constexpr (!overlaps<MODE, PLAIN>()) {
-    // 4 KiB tiles over the payload (reconstruct) or up to the object's end
-    const int64_t lim = MODE == kReconstruct ? static_cast<int64_t>(p.bs)
-                                             : last_room(p.bs, p.obj_len, K);
-    p.tiles = static_cast<uint32_t>(lim / tile);
-    p.edge_tiles = (p.bs + tile - 1) / tile - p.tiles;
-  } else {
-    // tile T covers loads [T*4032, T*4032 + 4048) and slice bytes up to
-    // T*4032 + 4048 - s; it must stay inside min(bs, room)
-    const int64_t lim = last_room(p.bs, p.obj_len, K);
-    p.tiles = lim >= tile + 16 ? static_cast<uint32_t>((lim - 16) / tile) : 0u;
-    p.edge_tiles = 1 + (p.bs - p.tiles * tile + 4095) / 4096;  // head + tail items
-  }
-  const uint32_t items = std::max(std::max(p.n_obj * p.tiles, p.n_obj * p.edge_tiles),
-                                  p.reconstruct ? p.n_obj : 0u);
-  return launch(decode_kernel<F, K, MODE, OCC, PLAIN, POL, STAGED, NOCOMP>, p,
-                decode_lds_bytes<F, K, STAGED>(), items, stream);
-}
-
+// Decode / reconstruct: (reconstruct headers +) edge items, then the
+// interior stream.  A multi-pass decode runs each pass as a decode (the
+// descriptor's copy_inputs / n_out say what the pass stores).
+// ECAMD_DEC_NOCOMP=1: memory-only probe of the benchmark shape.
 template <class F, int K, int MODE>
 hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
-  if constexpr (K == 10 && MODE == kDecode) {
-    if (env_flag("ECAMD_DEC_NOCOMP", false))  // memory-only probe (wrong output)
-      return env_flag("ECAMD_DEC_STAGED", kDecodeStaged)
-                 ? launch_decode_variant<F, K, MODE, 3, true, 0, true, true>(p, stream)
-                 : launch_decode_variant<F, K, MODE, kDecodeOcc, true, 0, false, true>(p, stream);
+  if constexpr (MODE == kDecodeGeneric) {
+    return launch_decode_mode<F, K, kDecode>(p, stream);
+  } else {
+    const int64_t lim = MODE == kReconstruct ? static_cast<int64_t>(p.bs)
+                                             : last_room(p.bs, p.obj_len, K);
+    p.tiles = static_cast<uint32_t>(lim / kTile);
+    p.edge_tiles = (p.bs + kTile - 1) / kTile - p.tiles;
+    constexpr size_t lds = decode_lds_bytes<F, K>();
+    const uint32_t edge_items =
+        std::max(p.n_obj * p.edge_tiles, MODE == kReconstruct && p.headers ? p.n_obj : 0u);
+    hipError_t e = launch(decode_edge_kernel<F, K, MODE>, p, lds, edge_items, stream);
+    if (e != hipSuccess) return e;
+    if constexpr (K == 10 && MODE == kDecode)
+      if (env_flag("ECAMD_DEC_NOCOMP", false))
+        return launch(decode_kernel<F, K, MODE, true>, p, lds, p.n_obj * p.tiles, stream,
+                      kDecodePerCu);
+    return launch(decode_kernel<F, K, MODE>, p, lds, p.n_obj * p.tiles, stream, kDecodePerCu);
   }
-  if constexpr (MODE == kDecode && staged_fits<F, K>()) {
-    // staged, line-friendly object stores (LDS bounds occupancy to 3 blocks
-    // per CU at k = 10, so the register budget is 3 waves per SIMD)
-    if (env_flag("ECAMD_DEC_STAGED", kDecodeStaged))
-      return launch_decode_variant<F, K, MODE, 3, true, 0, true>(p, stream);
-  }
-  if constexpr (K == 10 && MODE == kDecode) {
-    // the benchmark configuration carries the A/B variants
-    // (tools/ab_bench.py): ECAMD_DEC_OCC3=1 (3 waves per SIMD, no spills),
-    // ECAMD_DEC_PLAIN=1 (unaligned lane stores, no overlap lane)
-    const bool plain = env_flag("ECAMD_DEC_PLAIN", kDecodePlain);
-    switch (env_policy(0)) {
-      case 1:
-        return plain ? launch_decode_variant<F, K, MODE, kDecodeOcc, true, 1>(p, stream)
-                     : launch_decode_variant<F, K, MODE, kDecodeOcc, false, 1>(p, stream);
-      case 2:
-        return plain ? launch_decode_variant<F, K, MODE, kDecodeOcc, true, 2>(p, stream)
-                     : launch_decode_variant<F, K, MODE, kDecodeOcc, false, 2>(p, stream);
-      case 3:
-        return plain ? launch_decode_variant<F, K, MODE, kDecodeOcc, true, 3>(p, stream)
-                     : launch_decode_variant<F, K, MODE, kDecodeOcc, false, 3>(p, stream);
-      default:
-        break;
-    }
-    if (!plain) return launch_decode_variant<F, K, MODE, kDecodeOcc, false>(p, stream);
-    if (env_flag("ECAMD_DEC_OCC3", false))
-      return launch_decode_variant<F, K, MODE, 3, true>(p, stream);
-  }
-  return launch_decode_variant<F, K, MODE, kDecodeOcc, kDecodePlain>(p, stream);
 }
 
 }  // namespace

@@ -65,7 +65,7 @@ const Code* code_of(int backend_id) {
   }
 }
 constexpr int kRing = 4;
-constexpr int kHostStreams = 3;  // host-resident pipeline depth (H2D / kernel / D2H)
+constexpr int kHostStreams = 4;  // host-resident pipeline streams (H2D / kernel / D2H in flight)
 
 inline uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
@@ -85,6 +85,11 @@ inline uint64_t get64(const void* p) {
 bool env_on(const char* name) {
   const char* v = std::getenv(name);
   return v != nullptr && v[0] != 0 && v[0] != '0';
+}
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return (v == nullptr || *v == 0) ? dflt : std::atoi(v);
 }
 
 bool write_legacy_crc() {
@@ -893,12 +898,16 @@ bool device_mapped(const void* p, uint64_t n) {
 
 template <class Run>
 int host_pipeline(Instance& I, int n_obj, const HostSide& H, Run run) {
-  // ECAMD_HOST_DIRECT=1 (experiment): when both host arrays are pinned and
-  // mapped, run the kernels on them directly -- every load and store crosses
-  // PCIe from the CUs, no staging copies -- in one launch on one stream.
+  // Both host arrays pinned and mapped (the default path): the kernels run
+  // on them directly -- every load and store crosses PCIe from the CUs, no
+  // staging copies -- in one launch on one stream.  Measured round 2
+  // (tools/host_ab.py, k=10 m=4, 256 x 4 MiB): encode 50.4 GiB/s, decode
+  // 40.5, against 39.7 / 27.4 for the copy-engine pipeline below (whose
+  // H2D and D2H copies, run together, reach only 36 GiB/s each way).
+  // ECAMD_HOST_STAGED=1 forces the copy-engine pipeline.
   const uint64_t in_total = static_cast<uint64_t>(n_obj - 1) * H.in_stride + H.in_last;
   const uint64_t out_total = static_cast<uint64_t>(n_obj - 1) * H.out_stride + H.out_last;
-  if (env_on("ECAMD_HOST_DIRECT") && device_mapped(H.in, in_total) &&
+  if (!env_on("ECAMD_HOST_STAGED") && device_mapped(H.in, in_total) &&
       device_mapped(H.out, out_total)) {
     if (!I.hstream[0]) {
       hipError_t e = hipStreamCreateWithFlags(&I.hstream[0], hipStreamNonBlocking);
@@ -908,21 +917,24 @@ int host_pipeline(Instance& I, int n_obj, const HostSide& H, Run run) {
     const hipError_t e = hipStreamSynchronize(I.hstream[0]);
     return rc < 0 ? rc : (e == hipSuccess ? 0 : hip_errno(e));
   }
-  // Outputs: when the host output array is pinned and mapped, the kernels
-  // write it directly over PCIe (posted writes) while the copy engine moves
-  // the next chunks' inputs H2D -- the two directions of the link then run
-  // concurrently instead of queueing on the copy engines (measured round 2:
-  // staged D2H serialised behind H2D, encode 40 GiB/s = link / 1.4).
-  // ECAMD_HOST_STAGED_OUT=1 stages outputs through HBM + D2H copies instead.
+  // Otherwise chunks go H2D (copy engine) -> kernels -> host.  Outputs: when
+  // the host output array is pinned and mapped, the kernels write it
+  // directly over PCIe (posted writes) while the copy engine moves the next
+  // chunks' inputs H2D; ECAMD_HOST_STAGED_OUT=1 stages outputs through HBM +
+  // D2H copies instead (measured round 2: 44.8 / 30.4 GiB/s vs 39.7 / 27.4
+  // direct-out, both below the direct path above).
   const bool out_direct = !env_on("ECAMD_HOST_STAGED_OUT") && device_mapped(H.out, out_total);
-  // ~32 MiB of input per chunk, at least kHostStreams * 2 chunks when the
-  // batch allows, so the three stages overlap for most of the batch
-  int chunk = static_cast<int>(std::max<uint64_t>(1, (uint64_t(32) << 20) / H.in_stride));
-  chunk = std::min(chunk, std::max(1, (n_obj + 2 * kHostStreams - 1) / (2 * kHostStreams)));
+  // ~32 MiB of input per chunk, at least 2 chunks per stream when the batch
+  // allows, so the three stages overlap for most of the batch.
+  // ECAMD_HOST_CHUNK_MB / ECAMD_HOST_STREAMS: tuning knobs (tools/host_ab.py).
+  const int nstreams = std::max(1, std::min(kHostStreams, env_int("ECAMD_HOST_STREAMS", 3)));
+  const uint64_t chunk_bytes = static_cast<uint64_t>(std::max(1, env_int("ECAMD_HOST_CHUNK_MB", 32))) << 20;
+  int chunk = static_cast<int>(std::max<uint64_t>(1, chunk_bytes / H.in_stride));
+  chunk = std::min(chunk, std::max(1, (n_obj + 2 * nstreams - 1) / (2 * nstreams)));
   const uint64_t in_cap = (static_cast<uint64_t>(chunk) * H.in_stride + H.in_skew + 255) & ~255ull;
   const uint64_t out_cap = out_direct ? 0 : static_cast<uint64_t>(chunk) * H.out_stride + H.out_skew;
   hipError_t e = hipSuccess;
-  for (int s = 0; s < kHostStreams; ++s) {
+  for (int s = 0; s < nstreams; ++s) {
     if (!I.hstream[s] &&
         (e = hipStreamCreateWithFlags(&I.hstream[s], hipStreamNonBlocking)) != hipSuccess)
       return hip_errno(e);
@@ -931,7 +943,7 @@ int host_pipeline(Instance& I, int n_obj, const HostSide& H, Run run) {
   int rc = 0;
   for (int o0 = 0, c = 0; o0 < n_obj && rc == 0; o0 += chunk, ++c) {
     const int n = std::min(chunk, n_obj - o0);
-    const int si = c % kHostStreams;
+    const int si = c % nstreams;
     hipStream_t s = I.hstream[si];
     uint8_t* d_in = I.hbuf[si].b() + H.in_skew;
     uint8_t* d_out = out_direct ? H.out + static_cast<uint64_t>(o0) * H.out_stride

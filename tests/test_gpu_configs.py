@@ -125,11 +125,19 @@ def test_decode_pool_recycles_safely(gpu, oracle, monkeypatch):
                                            ("amd_rs_vand", 12, 4, 999999),
                                            ("isa_l_rs_cauchy", 12, 4, 1 << 20),
                                            ("amd_rs_vand", 4, 2, 17)])
-def test_host_resident_encode_decode_reconstruct(gpu, oracle, ec_type, k, m, n):
+@pytest.mark.parametrize("path", ["direct", "staged", "staged_out"])
+def test_host_resident_encode_decode_reconstruct(gpu, oracle, monkeypatch, ec_type, k, m, n,
+                                                 path):
     """ecamd_{encode,decode,reconstruct}_host_batch: pinned host in and out,
-    against the oracle (encode, reconstruct) and the objects (decode)."""
+    against the oracle (encode, reconstruct) and the objects (decode).  Paths:
+    kernels on the mapped host arrays (default), the copy-engine pipeline with
+    kernels writing host outputs, and the pipeline with D2H-staged outputs."""
     import torch
     from pyeclib_amd import batch
+    if path != "direct":
+        monkeypatch.setenv("ECAMD_HOST_STAGED", "1")
+    if path == "staged_out":
+        monkeypatch.setenv("ECAMD_HOST_STAGED_OUT", "1")
     B = 13
     host, masks, dests = _inputs(B, n, k, m, m, 97 + n)
     codec = batch.BatchCodec(k, m, ec_type=ec_type)

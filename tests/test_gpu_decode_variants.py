@@ -1,13 +1,12 @@
-"""GPU decode store variants: every object-store scheme of the decode kernel
-(ec_kernels_impl.hpp: lane-natural stores, and the LDS-staged 16-B-aligned
-stores chosen by ECAMD_DEC_STAGED) must rebuild the objects bit-exactly and
-write nothing outside [0, obj_len) of each object's output row.
+"""GPU decode object stores: the streaming decode kernel's slice stores (every
+slice alignment: 16-B aligned, 8 mod 16, odd for GF(2^8)), its dropped stores
+(parity inputs, rows past the missing count) and the edge items must rebuild
+the objects bit-exactly and write nothing outside [0, obj_len) of each
+object's output row.
 
-The switch is read at every launch, so both schemes run in this process on
-the same fragments.  Encode parity itself is pinned against the oracle in
-test_gpu_parity.py; here the decoded bytes are compared with the objects.
+Encode parity itself is pinned against the oracle in test_gpu_parity.py;
+here the decoded bytes are compared with the objects.
 """
-import os
 import random
 
 import numpy as np
@@ -31,8 +30,7 @@ CASES = [
 
 
 @pytest.mark.parametrize("ec_type,k,m,obj_len", CASES)
-@pytest.mark.parametrize("staged", ["0", "1"])
-def test_decode_store_schemes(gpu, ec_type, k, m, obj_len, staged):
+def test_decode_object_stores(gpu, ec_type, k, m, obj_len):
     import torch
     from pyeclib_amd import batch
     n_obj = 6
@@ -49,16 +47,8 @@ def test_decode_store_schemes(gpu, ec_type, k, m, obj_len, staged):
     masks = [full & ~sum(1 << i for i in rng.sample(range(k + m), o % (m + 1)))
              for o in range(n_obj)]
     out = torch.full((n_obj, stride), 0xA5, dtype=torch.uint8, device=gpu)
-    old = os.environ.get("ECAMD_DEC_STAGED")
-    os.environ["ECAMD_DEC_STAGED"] = staged
-    try:
-        codec.decode(stripes, obj_len, masks, out)
-        torch.cuda.synchronize()
-    finally:
-        if old is None:
-            del os.environ["ECAMD_DEC_STAGED"]
-        else:
-            os.environ["ECAMD_DEC_STAGED"] = old
+    codec.decode(stripes, obj_len, masks, out)
+    torch.cuda.synchronize()
     for o in range(n_obj):
         assert torch.equal(out[o, :obj_len], objs[o, :obj_len]), f"object {o} mask {masks[o]:x}"
         tail = out[o, obj_len:].cpu().numpy()
