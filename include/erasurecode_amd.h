@@ -193,9 +193,12 @@ int ecamd_reconstruct_batch(int desc, const void *d_frags, uint64_t frag_stride,
                             const uint32_t *h_avail, const int *h_dest, void *d_out,
                             uint64_t out_stride, void *stream);
 
-/* Host-resident encode: objects in (pinned) host memory, parity fragments
- * written back to host memory; H2D / kernel / D2H pipelined over chunks of
- * objects on three streams.  Synchronous.  Parity fragment p of object o at
+/* Host-resident encode: objects in host memory, parity fragments written
+ * back to host memory.  Synchronous.  When both host arrays are pinned
+ * (hipHostMalloc / hipHostRegister, device-mapped) the kernels read and write
+ * them directly over PCIe; otherwise chunks of objects are copied H2D on three
+ * streams, kernels write the outputs (pinned) or HBM + D2H copies (pageable).
+ * Parity fragment p of object o at
  * h_parity + (o*m + p)*frag_stride; objects as in ecamd_encode_batch.
  * Replaces, for a batch, the host side of pyeclib_c_encode
  * (src/pyeclib_c/pyeclib_c.c:512-565): bytes in, fragments out. */
@@ -209,7 +212,7 @@ int ecamd_encode_host_batch(int desc, const void *h_objs, uint64_t obj_stride, u
  *   h_avail:  n_obj bitmasks; the k lowest set bits name the fragments in
  *             h_frags (liberasurecode uses the first k available)
  *   h_objs:   output, object o at h_objs + o*obj_stride (obj_len bytes)
- * Pipelined like ecamd_encode_host_batch; synchronous.  Replaces, for a
+ * Paths as ecamd_encode_host_batch; synchronous.  Replaces, for a
  * batch, pyeclib_c_decode (src/pyeclib_c/pyeclib_c.c:770-922). */
 int ecamd_decode_host_batch(int desc, const void *h_frags, uint64_t frag_stride, uint64_t obj_len,
                             int n_obj, const uint32_t *h_avail, void *h_objs,
