@@ -388,6 +388,53 @@ def host_resident(args, codec, host, stripes, masks, fs, bs, reps=3):
     return out
 
 
+# ---------------- single-object calls (the ECDriver path Swift uses) ----------------
+
+def single_object_calls(args, sizes=(64 << 10, 1 << 20, 4 << 20), reps=20):
+    """Per-call latency of ECDriver.encode / decode (one object, pageable Python
+    bytes in and out: pyeclib_c.c:512-565 / :770-922 through the C ABI) and of
+    the scalar oracle on the same object, median of `reps` calls.  Decode drops
+    the first `erasures` data fragments, so it runs the GPU path, not the
+    concatenation fast path."""
+    from pyeclib_amd import ECDriver
+    k, m = args.k, args.m
+    ec_type = "liberasurecode_rs_vand" if args.ec_type == "amd_rs_vand" else args.ec_type
+    drv = ECDriver(k=k, m=m, ec_type=ec_type)
+    rng = np.random.Generator(np.random.PCG64(SEED + 7))
+    res = {}
+    for n in sizes:
+        data = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        frags = drv.encode(data)
+        lost = min(args.erasures, m)
+        avail = frags[lost:lost + k]
+        assert drv.decode(avail) == data, "single-object decode mismatch"
+        te, td = [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            drv.encode(data)
+            t1 = time.perf_counter()
+            drv.decode(avail)
+            t2 = time.perf_counter()
+            te.append(t1 - t0)
+            td.append(t2 - t1)
+        oc = OracleCodec(args.ec_type, k, m, n)
+        arr = np.frombuffer(data, dtype=np.uint8)
+        ce = [oc.encode(arr) for _ in range(3)]
+        mask = ((1 << (k + m)) - 1) & ~((1 << lost) - 1)
+        cd = [oc.decode(mask) for _ in range(3)]
+        res[f"{n >> 10}KiB"] = {
+            "gpu_encode_us": round(1e6 * float(np.median(te)), 1),
+            "gpu_decode_us": round(1e6 * float(np.median(td)), 1),
+            "oracle_encode_us": round(1e6 * float(np.median(ce)), 1),
+            "oracle_decode_us": round(1e6 * float(np.median(cd)), 1),
+        }
+    drv.close()
+    return {"single_object_calls": res,
+            "single_object_note": f"ECDriver({k},{m},{ec_type}) per-call latency, pageable bytes "
+                                  f"in/out, median of {reps}; decode with {min(args.erasures, m)} "
+                                  "data fragments missing; oracle = scalar C restatement, 1 core"}
+
+
 # ---------------- main ----------------
 
 def dry_run(args):
@@ -569,6 +616,7 @@ def main():
 
     if rank == 0 and not args.no_host and w == 16:
         result.update(host_resident(args, codec, host, stripes, masks, fs, bs))
+        result.update(single_object_calls(args))
 
     if rank == 0 and not args.no_cpu_baseline:
         sample = min(args.cpu_sample or B, B)

@@ -40,6 +40,8 @@ __host__ __device__ constexpr uint32_t table_slot_bytes(uint32_t k, uint32_t w) 
 }
 
 // ECAMD_XCD=0 turns off the XCD-major work split (every kernel).
+// ECAMD_EDGE_SIDE=1 runs the edge items in a launch of their own on a side
+// stream (the round-2 variant, for A/B runs) instead of in the interior launch.
 // ECAMD_ENC_NOCOMP=1 / ECAMD_DEC_NOCOMP=1: memory-only probes of the
 // benchmark case (k = 10; wrong output), read at each launch so
 // tools/ab_bench.py can time them beside the real kernels in one process.
@@ -60,6 +62,7 @@ struct EncodeParams {
   uint32_t n_obj;
   uint32_t tiles, edge_tiles;  // set by the launcher: interior / edge items per object
   uint32_t xcd_split;          // set by the launcher (item_range)
+  uint32_t fused_edges;        // set by the launcher: edge items run in the interior launch
 };
 
 // Per-object decode / reconstruct descriptor (device memory).
@@ -97,6 +100,7 @@ struct DecodeParams {
                             // 2 = generic (multi-pass decode)
   uint32_t tiles, edge_tiles;  // set by the launcher: interior / edge items per object
   uint32_t xcd_split;          // set by the launcher (item_range)
+  uint32_t fused_edges;        // set by the launcher: edge items run in the interior launch
 };
 
 // Dispatch on (p.w, p.k) to the per-k instantiations (ec_dispatch.cpp).

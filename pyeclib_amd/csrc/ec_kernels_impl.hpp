@@ -353,12 +353,39 @@ __device__ __forceinline__ uint32_t wave_in_block() {
 }
 
 // 16 bytes at base+off; bytes at or past `len` read as zero (encode padding).
+// Two 16-B loads at 16-B-aligned offsets inside [0, round16(len)) -- the
+// object's buffer spans at least that (obj_stride is a multiple of 16 and
+// >= len) -- funnel-shifted into place: no byte loads, 8 VGPRs per input,
+// whatever the alignment of off.
 __device__ __forceinline__ uint4 load_clamped(const uint8_t* base, uint64_t off, uint64_t len) {
-  if (off + 16 <= len) return *reinterpret_cast<const uint4*>(base + off);
-  uint32_t w[4] = {0, 0, 0, 0};
-  for (int i = 0; i < 16; ++i)
-    if (off + i < len) w[i >> 2] |= static_cast<uint32_t>(base[off + i]) << (8 * (i & 3));
-  return make_uint4(w[0], w[1], w[2], w[3]);
+  // len > 0 (no edge item runs for an empty object); branch-free: units past
+  // the last one holding object bytes are read from that one and masked off
+  const uint64_t last = (len - 1) & ~uint64_t(15);
+  const uint64_t a = off & ~uint64_t(15);
+  const uint64_t a0 = a < last ? a : last;
+  const uint64_t a1 = a0 + 16 <= last ? a0 + 16 : a0;
+  const uint4 u = *reinterpret_cast<const uint4*>(base + a0);
+  const uint4 v = *reinterpret_cast<const uint4*>(base + a1);
+  const uint32_t s = static_cast<uint32_t>(off & 15);
+  uint32_t w[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+  if (s & 8) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) w[i] = w[i + 2];
+  }
+  if (s & 4) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) w[i] = w[i + 1];
+  }
+  uint32_t r[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], s & 3);
+  const int64_t n = static_cast<int64_t>(len) - static_cast<int64_t>(off);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t valid = n - 4 * i;
+    r[i] &= valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : (1u << (8 * valid)) - 1u);
+  }
+  return make_uint4(r[0], r[1], r[2], r[3]);
 }
 
 __device__ __forceinline__ uint32_t byte_of(const uint4& v, uint32_t b) {
@@ -502,6 +529,10 @@ __device__ __forceinline__ void enc_item_pos(const EncodeParams& p, uint32_t w, 
   x = (w - o * p.tiles) * kTile + wave_in_block() * kChunkBytes;
 }
 
+// Inputs an edge item holds in registers at once (edge items run inside the
+// streaming kernels, ahead of their interior items).
+constexpr int kEdgeGroup = 1;
+
 // Edge item: payload tail and chunks reaching the zero padding past obj_len
 // (liberasurecode's prepare_fragments_for_encode zero-fills).
 template <class F, int K, int NR>
@@ -511,13 +542,23 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
   if (t >= p.bs) return;
   const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride;
   const int64_t rem = static_cast<int64_t>(p.bs) - t;
-  uint4 x[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) x[j] = load_clamped(obj, static_cast<uint64_t>(j) * p.bs + t, p.obj_len);
+  // kEdgeGroup inputs in registers at a time, the groups fenced off from
+  // each other: this runs inside the streaming kernel (encode_edges), whose
+  // register budget it must not raise
   typename F::Acc s;
   F::zero(s);
 #pragma unroll
-  for (int j = 0; j < K; ++j) F::template mac<true>(F::kb(0), j * F::kTableBytes, x[j], s);
+  for (int j0 = 0; j0 < K; j0 += kEdgeGroup) {
+    constexpr int G = kEdgeGroup;
+    uint4 x[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+      if (j0 + j < K) x[j] = load_clamped(obj, static_cast<uint64_t>(j0 + j) * p.bs + t, p.obj_len);
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+      if (j0 + j < K) F::template mac<true>(F::kb(0), (j0 + j) * F::kTableBytes, x[j], s);
+    __builtin_amdgcn_sched_barrier(0);
+  }
   F::pin(s);
   uint8_t* par = p.parity + static_cast<uint64_t>(o) * p.stripe_stride + p.row0 * p.frag_stride +
                  kHeaderBytes + t;
@@ -530,11 +571,8 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
 // chunks stored nontemporal and line-aligned.  NOCOMP: memory-only probe
 // (inputs XORed, no lookups; wrong parity) for the benchmark shape.
 template <class F, int K, int NR, bool NOCOMP = false>
-__global__ void __launch_bounds__(kThreadsPerBlock)
-    __attribute__((amdgpu_waves_per_eu(kEncodeOcc, 8))) encode_kernel(EncodeParams p) {
+__device__ __forceinline__ void encode_interior(const EncodeParams& p) {
   constexpr int NB = stream_bufs<K>();
-  load_tables(p.tables, K * F::kTableBytes, 0);
-  __syncthreads();
   const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
   uint32_t w = r.begin;
   if (w >= r.end) return;
@@ -582,21 +620,42 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
   }
 }
 
-// Headers and edge items of an encode: a launch of their own, so their
-// registers (all K edge inputs at once) do not bound the interior loop's
-// occupancy.
+// Headers and edge items of an encode, block b taking objects / items
+// b, b + G, ... (b counted from `first`, G = `step` blocks).  Tables are at LDS 0.
 template <class F, int K, int NR>
-__global__ void __launch_bounds__(kThreadsPerBlock) encode_edge_kernel(EncodeParams p) {
-  load_tables(p.tables, K * F::kTableBytes, 0);
+__device__ __forceinline__ void encode_edges(const EncodeParams& p, uint32_t first, uint32_t step) {
   if (p.headers != nullptr && p.row0 == 0)
-    for (uint32_t o = blockIdx.x; o < p.n_obj; o += gridDim.x) {
+    for (uint32_t o = first; o < p.n_obj; o += step) {
       const uint64_t base = static_cast<uint64_t>(o) * p.stripe_stride;
       block_headers(p.parity + base, p.frag_stride, p.headers + K * kHeaderBytes, p.m);
       if (p.data != nullptr) block_headers(p.data + base, p.frag_stride, p.headers, K);
     }
+  for (uint32_t e = first; e < p.n_obj * p.edge_tiles; e += step) encode_edge_item<F, K, NR>(p, e);
+}
+
+// One launch per encode: the headers and edge items, in the blocks counted
+// from the END of the grid -- which hold one interior item fewer whenever the
+// items do not divide evenly, so the edge latency is absorbed -- then the
+// interior stream.  Measured round 2 (rocprof timeline,
+// profiles/r02l_timeline.txt): with the edges in a launch of their own on a
+// side stream, the fork / join left the GPU idle 25-32 us between
+// consecutive interior kernels.
+template <class F, int K, int NR, bool NOCOMP = false>
+__global__ void __launch_bounds__(kThreadsPerBlock)
+    __attribute__((amdgpu_waves_per_eu(kEncodeOcc, 8))) encode_kernel(EncodeParams p) {
+  load_tables(p.tables, K * F::kTableBytes, 0);
   __syncthreads();
-  for (uint32_t e = blockIdx.x; e < p.n_obj * p.edge_tiles; e += gridDim.x)
-    encode_edge_item<F, K, NR>(p, e);
+  if (p.fused_edges) encode_edges<F, K, NR>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
+  encode_interior<F, K, NR, NOCOMP>(p);
+}
+
+// Headers and edge items of an encode in a launch of their own (the
+// side-stream variant, ECAMD_EDGE_SIDE=1, kept for A/B runs).
+template <class F, int K, int NR>
+__global__ void __launch_bounds__(kThreadsPerBlock) encode_edge_kernel(EncodeParams p) {
+  load_tables(p.tables, K * F::kTableBytes, 0);
+  __syncthreads();
+  encode_edges<F, K, NR>(p, blockIdx.x, gridDim.x);
 }
 
 // Data fragments (optional output of encode): the k padded object slices
@@ -768,11 +827,9 @@ __device__ __forceinline__ Rsrc rsrc_out(const void* base) {
 // kDrop and are discarded by the range check, so every item issues the same
 // memory instructions.  NOCOMP: memory-only probe (no lookups; wrong rows).
 template <class F, int K, int MODE, bool NOCOMP = false>
-__global__ void __launch_bounds__(kThreadsPerBlock)
-    __attribute__((amdgpu_waves_per_eu(kDecodeOcc, 8))) decode_kernel(DecodeParams p) {
+__device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st,
+                                                TablePre<F, K>& pre) {
   constexpr int NB = stream_bufs<K>();
-  Slots st{0xFFFFFFFFu, 1u};
-  TablePre<F, K> pre;
   const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
   uint32_t w = r.begin;
   if (w >= r.end) return;  // block-uniform: no wave of this block reaches a barrier
@@ -850,29 +907,38 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
   uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
   // t < bs and 16 | t, so t + 16 <= round16(bs) <= frag_stride - 80: in bounds
   const uint8_t* in = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
-  uint4 x[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j)
-    x[j] = *reinterpret_cast<const uint4*>(in + in_pos(p, d, j) * p.frag_stride);
+  // kEdgeGroup inputs in registers at a time (this runs inside the streaming
+  // kernel, decode_edges: see encode_edge_item)
   typename F::Acc s;
   F::zero(s);
-  if (d.n_out() != 0) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) F::mac(kb, j * F::kTableBytes, x[j], s);
+  for (int j0 = 0; j0 < K; j0 += kEdgeGroup) {
+    constexpr int G = kEdgeGroup;
+    uint4 x[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+      if (j0 + j < K) x[j] = *reinterpret_cast<const uint4*>(in + in_pos(p, d, j0 + j) * p.frag_stride);
+    if (d.n_out() != 0) {
+#pragma unroll
+      for (int j = 0; j < G; ++j)
+        if (j0 + j < K) F::mac(kb, (j0 + j) * F::kTableBytes, x[j], s);
+    }
+    if (MODE != kReconstruct && d.copy_inputs()) {
+#pragma unroll
+      for (int j = 0; j < G; ++j) {
+        if (j0 + j >= K) continue;
+        const uint32_t idx = d.in_idx(j0 + j);
+        if (idx >= K) continue;
+        store_window(out + static_cast<uint64_t>(idx) * p.bs, t, x[j], tail0,
+                     object_bytes(idx, p.bs, 0, p.obj_len));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
   }
   F::pin(s);
   if (MODE == kReconstruct) {
     if (d.n_out() != 0) store_window(out + kHeaderBytes, t, F::row(s, 0), tail0, p.bs);
     return;
-  }
-  if (d.copy_inputs()) {
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const uint32_t idx = d.in_idx(j);
-      if (idx >= K) continue;
-      store_window(out + static_cast<uint64_t>(idx) * p.bs, t, x[j], tail0,
-                   object_bytes(idx, p.bs, 0, p.obj_len));
-    }
   }
   for (uint32_t q = 0; q < d.n_out(); ++q) {
     const uint32_t idx = d.out_idx(q);
@@ -881,19 +947,40 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
   }
 }
 
-// Reconstruct headers and the edge items of a decode / reconstruct (own
-// launch, own registers).
+// Reconstruct headers and the edge items of a decode / reconstruct, block b
+// taking objects / items b, b + G, ... (b counted from `first`, G = `step`).
+// Block-uniform (ensure_tables has a barrier).
 template <class F, int K, int MODE>
-__global__ void __launch_bounds__(kThreadsPerBlock) decode_edge_kernel(DecodeParams p) {
+__device__ __forceinline__ void decode_edges(const DecodeParams& p, uint32_t first, uint32_t step,
+                                             Slots& st, TablePre<F, K>& pre) {
   if (MODE == kReconstruct && p.headers != nullptr)
-    for (uint32_t o = blockIdx.x; o < p.n_obj; o += gridDim.x)
+    for (uint32_t o = first; o < p.n_obj; o += step)
       block_headers(p.out + static_cast<uint64_t>(o) * p.out_stride, 0,
                     p.headers + static_cast<uint64_t>(load_desc(p, o).header()) * kHeaderBytes, 1);
+  pre.table = 0xFFFFFFFFu;
+  for (uint32_t e = first; e < p.n_obj * p.edge_tiles; e += step)
+    decode_edge_item<F, K, MODE>(p, e, st, pre);
+}
+
+// One launch per decode / reconstruct pass: the edge items in the blocks
+// counted from the end of the grid (see encode_kernel), then the interior
+// stream.  The interior's first table change goes into the LDS slot the edge
+// items did not use, behind a barrier, as between any two items.
+template <class F, int K, int MODE, bool NOCOMP = false>
+__global__ void __launch_bounds__(kThreadsPerBlock)
+    __attribute__((amdgpu_waves_per_eu(kDecodeOcc, 8))) decode_kernel(DecodeParams p) {
   Slots st{0xFFFFFFFFu, 1u};
   TablePre<F, K> pre;
-  pre.table = 0xFFFFFFFFu;
-  for (uint32_t e = blockIdx.x; e < p.n_obj * p.edge_tiles; e += gridDim.x)
-    decode_edge_item<F, K, MODE>(p, e, st, pre);
+  if (p.fused_edges) decode_edges<F, K, MODE>(p, gridDim.x - 1 - blockIdx.x, gridDim.x, st, pre);
+  decode_interior<F, K, MODE, NOCOMP>(p, st, pre);
+}
+
+// The edge work in a launch of its own (side-stream variant, ECAMD_EDGE_SIDE=1).
+template <class F, int K, int MODE>
+__global__ void __launch_bounds__(kThreadsPerBlock) decode_edge_kernel(DecodeParams p) {
+  Slots st{0xFFFFFFFFu, 1u};
+  TablePre<F, K> pre;
+  decode_edges<F, K, MODE>(p, blockIdx.x, gridDim.x, st, pre);
 }
 
 // ---------------- launch ----------------
@@ -983,6 +1070,10 @@ hipError_t fork_join(hipStream_t stream, Main main, Side side) {
   std::lock_guard<std::mutex> lk(mu);
   int dev = 0;
   SideStream* sd = nullptr;
+  if (env_int("ECAMD_EDGE_SIDE", 0) == 2) {  // A/B: edge launch first, same stream
+    const hipError_t e = side(stream);
+    return e != hipSuccess ? e : main(stream);
+  }
   if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64) {
     sd = &per_dev[dev];
     if (sd->s == nullptr &&
@@ -1031,7 +1122,20 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     probe = env_flag("ECAMD_ENC_NOCOMP", false);
     per_cu = env_int("ECAMD_ENC_PER_CU", kEncodePerCu);  // A/B
   }
-  hipError_t e = fork_join(
+  hipError_t e;
+  if (!env_flag("ECAMD_EDGE_SIDE", false)) {
+    // one launch: interior stream + edge items + headers
+    p.fused_edges = 1;
+    const uint32_t items = std::max({p.n_obj * p.tiles, p.n_obj * p.edge_tiles,
+                                     p.headers ? p.n_obj : 0u});
+    if constexpr (K == 10 && NR == 4)
+      if (probe) return launch(encode_kernel<F, K, NR, true>, p, lds, items, stream, per_cu);
+    e = launch(encode_kernel<F, K, NR>, p, lds, items, stream, per_cu);
+    if (e != hipSuccess || p.data == nullptr || p.row0 != 0) return e;
+    return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + kTile - 1) / kTile), stream);
+  }
+  p.fused_edges = 0;
+  e = fork_join(
       stream,
       [&](hipStream_t s) {
         if constexpr (K == 10 && NR == 4)
@@ -1087,6 +1191,16 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
         std::max(p.n_obj * p.edge_tiles, MODE == kReconstruct && p.headers ? p.n_obj : 0u);
     bool probe = false;
     if constexpr (K == 10 && MODE == kDecode) probe = env_flag("ECAMD_DEC_NOCOMP", false);
+    if (!env_flag("ECAMD_EDGE_SIDE", false)) {
+      p.fused_edges = 1;
+      const uint32_t items = std::max(p.n_obj * p.tiles, edge_items);
+      if constexpr (K == 10 && MODE == kDecode)
+        if (probe)
+          return launch(decode_kernel<F, K, MODE, true>, p, lds, items, stream, kDecodePerCu,
+                        kDecodeXcd);
+      return launch(decode_kernel<F, K, MODE>, p, lds, items, stream, kDecodePerCu, kDecodeXcd);
+    }
+    p.fused_edges = 0;
     return fork_join(
         stream,
         [&](hipStream_t s) {

@@ -166,6 +166,50 @@ struct DevBuf {
   uint8_t* b() const { return static_cast<uint8_t*>(p); }
 };
 
+// Pinned, device-mapped host memory (same address on both sides) for the
+// single-object calls: the kernels read and write it over PCIe, the host
+// fills and drains it with memcpy -- no DMA copies, which from pageable
+// Python bytes cost a staged transfer each (one per fragment on decode).
+struct PinBuf {
+  uint8_t* p = nullptr;
+  size_t cap = 0;
+  bool failed = false;  // allocation or mapping refused: use the DMA path
+  uint8_t* ensure(size_t n) {
+    if (failed) return nullptr;
+    if (n <= cap) return p;
+    release();
+    const size_t want = std::max<size_t>((n + (1 << 20) - 1) & ~size_t((1 << 20) - 1), 1 << 20);
+    void* h = nullptr;
+    void* d = nullptr;
+    if (hipHostMalloc(&h, want, hipHostMallocMapped) != hipSuccess) {
+      (void)hipGetLastError();
+      failed = true;
+      return nullptr;
+    }
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || d != h) {
+      (void)hipGetLastError();
+      (void)hipHostFree(h);
+      failed = true;
+      return nullptr;
+    }
+    p = static_cast<uint8_t*>(h);
+    cap = want;
+    return p;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// Objects up to this many bytes take the zero-copy single-object path
+// (ECAMD_SINGLE_PINNED_MAX overrides; 0 turns it off).
+size_t single_pinned_max() {
+  const char* v = std::getenv("ECAMD_SINGLE_PINNED_MAX");
+  return (v == nullptr || *v == 0) ? (size_t(1) << 20) : static_cast<size_t>(std::atoll(v));
+}
+
 // Descriptor/header upload slot: pinned staging + device copy + completion event.
 struct RingSlot {
   uint8_t* host = nullptr;
@@ -230,6 +274,7 @@ struct Instance {
   uint64_t pool_gen = 1;  // bumped whenever slots are recycled
   std::unordered_map<uint64_t, uint32_t> pool_index;
   DevBuf scratch;  // single-object staging
+  PinBuf pin;      // single-object staging, zero-copy (small objects)
   RingSlot ring[kRing];
   int ring_pos = 0;
   UploadCache dec_cache, rec_cache, hdr_cache;
@@ -265,6 +310,7 @@ struct Instance {
     enc_tables.release();
     pool.release();
     scratch.release();
+    pin.release();
     for (auto& b : hbuf) b.release();
     for (auto& kv : crc_tables) kv.second.release();
     if (stream) (void)hipStreamDestroy(stream);
@@ -1083,21 +1129,30 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
   if (bs > 0) {
     const uint64_t fs = round16(kHeaderBytes + round16(bs));
     const uint64_t obj_bytes = round16(orig_data_size);
-    hipError_t e = I->scratch.ensure(obj_bytes + fs * m);
-    if (e != hipSuccess) return fail(hip_errno(e));
-    uint8_t* d_obj = I->scratch.b();
+    uint8_t* pin = orig_data_size <= single_pinned_max() ? I->pin.ensure(obj_bytes + fs * m)
+                                                         : nullptr;
+    hipError_t e = hipSuccess;
+    if (!pin && (e = I->scratch.ensure(obj_bytes + fs * m)) != hipSuccess)
+      return fail(hip_errno(e));
+    uint8_t* d_obj = pin ? pin : I->scratch.b();
     uint8_t* d_par = d_obj + obj_bytes;
-    if ((e = hipMemcpyAsync(d_obj, orig_data, orig_data_size, hipMemcpyHostToDevice,
-                            I->stream)) != hipSuccess)
+    if (pin)
+      std::memcpy(d_obj, orig_data, orig_data_size);
+    else if ((e = hipMemcpyAsync(d_obj, orig_data, orig_data_size, hipMemcpyHostToDevice,
+                                 I->stream)) != hipSuccess)
       return fail(hip_errno(e));
     int rc = run_encode(*I, d_obj, obj_bytes, orig_data_size, 1, d_par, nullptr, fs, fs * m,
                         false, I->stream);
     if (rc < 0) return fail(rc);
-    for (int p = 0; p < m; ++p)
-      if ((e = hipMemcpyAsync(par[p] + kHeaderBytes, d_par + p * fs + kHeaderBytes, bs,
-                              hipMemcpyDeviceToHost, I->stream)) != hipSuccess)
-        return fail(hip_errno(e));
+    if (!pin)
+      for (int p = 0; p < m; ++p)
+        if ((e = hipMemcpyAsync(par[p] + kHeaderBytes, d_par + p * fs + kHeaderBytes, bs,
+                                hipMemcpyDeviceToHost, I->stream)) != hipSuccess)
+          return fail(hip_errno(e));
     if ((e = hipStreamSynchronize(I->stream)) != hipSuccess) return fail(hip_errno(e));
+    if (pin)
+      for (int p = 0; p < m; ++p)
+        std::memcpy(par[p] + kHeaderBytes, d_par + p * fs + kHeaderBytes, bs);
   }
   for (int j = 0; j < k; ++j)
     make_header(reinterpret_cast<uint8_t*>(dat[j]), I->code, j, static_cast<uint32_t>(bs),
@@ -1170,12 +1225,19 @@ int partition(const Instance& I, char** frags, int n, Partition& P) {
 }
 
 // Upload the first k available payloads into a [k+m][fs] device image.
+// (`pinned`: d_frags is the zero-copy staging buffer, filled with memcpy.)
 int stage_fragments(Instance& I, const Partition& P, uint64_t bs, uint64_t fs, uint8_t* d_frags,
-                    uint32_t* mask) {
+                    uint32_t* mask, bool pinned) {
   int c = 0;
   *mask = 0;
   for (int i = 0; i < I.k + I.m && c < I.k; ++i) {
     if (!P.by_idx[i]) continue;
+    if (pinned) {
+      std::memcpy(d_frags + i * fs + kHeaderBytes, P.by_idx[i] + kHeaderBytes, bs);
+      *mask |= 1u << i;
+      ++c;
+      continue;
+    }
     hipError_t e = hipMemcpyAsync(d_frags + i * fs + kHeaderBytes, P.by_idx[i] + kHeaderBytes, bs,
                                   hipMemcpyHostToDevice, I.stream);
     if (e != hipSuccess) return hip_errno(e);
@@ -1249,23 +1311,26 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
   }
   const uint64_t fs = round16(kHeaderBytes + round16(bs));
   const uint64_t obj_bytes = round16(orig);
-  hipError_t e = I->scratch.ensure(fs * (k + I->m) + obj_bytes);
-  if (e != hipSuccess) {
+  const size_t need = fs * (k + I->m) + obj_bytes;
+  uint8_t* pin = orig <= single_pinned_max() ? I->pin.ensure(need) : nullptr;
+  hipError_t e = hipSuccess;
+  if (!pin && (e = I->scratch.ensure(need)) != hipSuccess) {
     std::free(out);
     return hip_errno(e);
   }
-  uint8_t* d_frags = I->scratch.b();
+  uint8_t* d_frags = pin ? pin : I->scratch.b();
   uint8_t* d_obj = d_frags + fs * (k + I->m);
   uint32_t mask = 0;
-  rc = stage_fragments(*I, P, bs, fs, d_frags, &mask);
+  rc = stage_fragments(*I, P, bs, fs, d_frags, &mask, pin != nullptr);
   if (rc == 0) {
     DecodeJob J{d_frags, fs, fs * (k + I->m), orig, d_obj, obj_bytes, 1, &mask, nullptr, nullptr};
     rc = run_decode(*I, J, I->stream);
   }
-  if (rc == 0 && orig)
+  if (rc == 0 && orig && !pin)
     if ((e = hipMemcpyAsync(out, d_obj, orig, hipMemcpyDeviceToHost, I->stream)) != hipSuccess)
       rc = hip_errno(e);
   if ((e = hipStreamSynchronize(I->stream)) != hipSuccess && rc == 0) rc = hip_errno(e);
+  if (rc == 0 && orig && pin) std::memcpy(out, d_obj, orig);
   if (rc < 0) {
     std::free(out);
     return rc;
@@ -1312,23 +1377,26 @@ int liberasurecode_reconstruct_fragment(int desc, char** available_fragments, in
   std::memset(out_fragment, 0, fragment_len);
   if (bs > 0) {
     const uint64_t fs = round16(kHeaderBytes + round16(bs));
-    hipError_t e = I->scratch.ensure(fs * (k + m + 1));
-    if (e != hipSuccess) return hip_errno(e);
-    uint8_t* d_frags = I->scratch.b();
+    const size_t need = fs * (k + m + 1);
+    uint8_t* pin = orig <= single_pinned_max() ? I->pin.ensure(need) : nullptr;
+    hipError_t e = hipSuccess;
+    if (!pin && (e = I->scratch.ensure(need)) != hipSuccess) return hip_errno(e);
+    uint8_t* d_frags = pin ? pin : I->scratch.b();
     uint8_t* d_out = d_frags + fs * (k + m);
     uint32_t mask = 0;
-    rc = stage_fragments(*I, P, bs, fs, d_frags, &mask);
+    rc = stage_fragments(*I, P, bs, fs, d_frags, &mask, pin != nullptr);
     if (rc == 0) {
       uint8_t hdr[kHeaderBytes] = {0};
       DecodeJob J{d_frags, fs, fs * (k + m), orig, d_out, fs, 1, &mask, &destination_idx, hdr};
       rc = run_decode(*I, J, I->stream);
     }
-    if (rc == 0 &&
+    if (rc == 0 && !pin &&
         (e = hipMemcpyAsync(out_fragment + kHeaderBytes, d_out + kHeaderBytes, bs,
                             hipMemcpyDeviceToHost, I->stream)) != hipSuccess)
       rc = hip_errno(e);
     if ((e = hipStreamSynchronize(I->stream)) != hipSuccess && rc == 0) rc = hip_errno(e);
     if (rc < 0) return rc;
+    if (pin) std::memcpy(out_fragment + kHeaderBytes, d_out + kHeaderBytes, bs);
   }
   make_header(reinterpret_cast<uint8_t*>(out_fragment), I->code, destination_idx,
               static_cast<uint32_t>(bs), orig, I->ct,

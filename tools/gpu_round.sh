@@ -28,6 +28,12 @@ for s in $STEPS; do
   ab)
     (cd $R && timeout -k 10 400 python3 tools/ab_bench.py ${AB:-base ECAMD_DEC_OCC3=1 ECAMD_XCD=0} > $O/ab.txt 2>&1)
     cat $O/ab.txt ;;
+  single)
+    (cd $R && timeout -k 10 300 python3 tools/single_ab.py > $O/single_ab.txt 2>&1)
+    cat $O/single_ab.txt ;;
+  timeline)
+    python3 $R/tools/rocpd_timeline.py $O/prof --last 24 > $O/timeline.txt 2>&1 || true
+    cat $O/timeline.txt ;;
   bench)
     (cd $R && timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err)
     cat $O/bench.json ;;
