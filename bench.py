@@ -498,36 +498,42 @@ def main():
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
+    p_parity = stripes[:, k:]
 
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        codec.encode(objs, n, parity=stripes[:, k:])
-        if ev is not None:
-            ev[1].record(stream)
+    # Kernel timing: HIP events on the launch stream, two per step -- before
+    # the encode and before the decode; a decode ends at the next step's first
+    # event (or the closing one).  (Each event record costs the stream ~5 us
+    # of GPU time between kernels: profiles/r02n_timeline.txt.)
+    def step(ev_enc=None, ev_dec=None):
+        if ev_enc is not None:
+            ev_enc.record(stream)
+        codec.encode(objs, n, parity=p_parity)
+        if ev_dec is not None:
+            ev_dec.record(stream)
         if two == "decode":
             codec.decode(stripes, n, masks, out)
         else:
             codec.reconstruct(stripes, n, rmasks, dests, rec)
-        if ev is not None:
-            ev[2].record(stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps + 1)]
     shard.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(events[i])
+        step(events[2 * i], events[2 * i + 1])
+    events[-1].record(stream)
     torch.cuda.synchronize()
     shard.barrier()
     elapsed = shard.max_over_ranks(time.perf_counter() - t0, device=dev)
 
-    enc_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in events]))
-    dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in events]))
+    enc_ms = float(np.mean([events[2 * i].elapsed_time(events[2 * i + 1])
+                            for i in range(args.steps)]))
+    dec_ms = float(np.mean([events[2 * i + 1].elapsed_time(events[2 * i + 2])
+                            for i in range(args.steps)]))
     step_s = elapsed / args.steps
     n_total = args.global_batch or B * world
     total_bytes = 2 * n_total * n

@@ -204,7 +204,12 @@ struct PinBuf {
 };
 
 // Objects up to this many bytes take the zero-copy single-object path
-// (ECAMD_SINGLE_PINNED_MAX overrides; 0 turns it off).
+// (ECAMD_SINGLE_PINNED_MAX overrides; 0 turns it off).  Measured round 2
+// (tools/single_ab.py, profiles/r02m_single_ab.txt and r02n, k=10 m=4):
+// faster than the DMA path up to 1 MiB on both boxes -- 64 KiB encode 51-54
+// vs 97-105 us, decode 57-59 vs 91-93; 1 MiB 148 vs 181-187, 163-167 vs
+// 264-268 -- and mixed at 4 MiB, where host-side copies and page faults
+// dominate either way.
 size_t single_pinned_max() {
   const char* v = std::getenv("ECAMD_SINGLE_PINNED_MAX");
   return (v == nullptr || *v == 0) ? (size_t(1) << 20) : static_cast<size_t>(std::atoll(v));
@@ -233,8 +238,6 @@ struct UploadCache {
   uint8_t* host = nullptr;
   size_t host_cap = 0;
   DevBuf dev;
-  hipEvent_t ev = nullptr;  // recorded after the last launch that read `dev`
-  bool pending = false;
   hipStream_t last_stream = nullptr;
   bool used = false;          // last_stream is meaningful
   hipEvent_t fill_ev = nullptr;     // recorded after the H2D copy that filled `dev`
@@ -242,11 +245,7 @@ struct UploadCache {
   bool fill_done = false;           // that copy is known to be complete
   bool multi_stream = false;  // read from more than one stream since filled
   void release() {
-    if (ev) {
-      (void)hipEventSynchronize(ev);
-      (void)hipEventDestroy(ev);
-      ev = nullptr;
-    }
+    if (used) (void)hipDeviceSynchronize();  // launches reading `dev` (no events)
     if (fill_ev) {
       (void)hipEventSynchronize(fill_ev);
       (void)hipEventDestroy(fill_ev);
@@ -385,17 +384,13 @@ int upload(Instance& I, UploadCache& C, const std::vector<uint8_t>& key, uint64_
   if (C.last_key == key && C.last_gen == gen) {
     // second call in a row with this key: make it resident, once no launch
     // can still be reading the old bytes
-    if (C.multi_stream) {
-      if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_errno(e);
-    } else if (C.pending) {
-      if ((e = hipEventSynchronize(C.ev)) != hipSuccess) return hip_errno(e);
-    }
-    C.pending = false;
+    // (launches that read the cache record no event -- an event record costs
+    // GPU time between kernels -- so a rewrite waits for the whole device; it
+    // happens once per new repeated key)
+    if (C.used && (e = hipDeviceSynchronize()) != hipSuccess) return hip_errno(e);
     C.multi_stream = false;
     C.used = false;
     C.dev_valid = false;
-    if (!C.ev && (e = hipEventCreateWithFlags(&C.ev, hipEventDisableTiming)) != hipSuccess)
-      return hip_errno(e);
     if (C.host_cap < n) {
       if (C.host) (void)hipHostFree(C.host);
       C.host = nullptr;
@@ -441,9 +436,7 @@ hipError_t upload_done(Instance& I, Upload& u, hipStream_t s) {
     if (C.used && C.last_stream != s) C.multi_stream = true;
     C.last_stream = s;
     C.used = true;
-    hipError_t e = hipEventRecord(C.ev, s);
-    C.pending = (e == hipSuccess);
-    return e;
+    return hipSuccess;
   }
   return hipSuccess;
 }
@@ -1012,10 +1005,11 @@ int host_pipeline(Instance& I, int n_obj, const HostSide& H, Run run) {
   return rc;
 }
 
-char* alloc_fragment(uint64_t size) {
+// zero = false: the caller writes every byte (decode's object buffer).
+char* alloc_fragment(uint64_t size, bool zero = true) {
   void* p = nullptr;
   if (posix_memalign(&p, 16, size ? size : 16) != 0) return nullptr;
-  std::memset(p, 0, size ? size : 16);
+  if (zero) std::memset(p, 0, size ? size : 16);
   return static_cast<char*>(p);
 }
 
@@ -1291,7 +1285,7 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
       break;
     }
   if (bs + kHeaderBytes > fragment_len) return -EBADHEADER;
-  char* out = static_cast<char*>(alloc_fragment(orig));
+  char* out = static_cast<char*>(alloc_fragment(orig, false));
   if (!out) return -ENOMEM;
   if (all_data && rc != -EBADHEADER) {
     // Fast path (fragments_to_string): every data fragment present, no GF work.
@@ -1301,6 +1295,7 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
       std::memcpy(out + off, P.by_idx[j] + kHeaderBytes, c);
       off += c;
     }
+    if (off < orig) std::memset(out + off, 0, orig - off);  // short size fields
     *out_data = out;
     *out_data_len = orig;
     return 0;
