@@ -81,6 +81,9 @@ def parse(argv=None):
     ap.add_argument("--second", default="decode", choices=["decode", "reconstruct"],
                     help="second half of a step: decode the batch, or rebuild one "
                          "random fragment per object")
+    ap.add_argument("--inline-crc32", action="store_true",
+                    help="chksum_type inline_crc32: every fragment header carries the zlib "
+                         "CRC-32 of its payload (core.py:59-63)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0,
                     help="objects in the CPU baseline sample (default: the full batch)")
@@ -135,9 +138,10 @@ class OracleCodec:
     """Raw-pointer view of the scalar C oracle for one (ec_type, k, m, L):
     each call returns the seconds spent inside the C function only."""
 
-    def __init__(self, ec_type, k, m, n):
+    def __init__(self, ec_type, k, m, n, crc=False):
         from oracle import oracle as O
         self.O, self.k, self.m, self.n = O, k, m, n
+        self.ct = O.CHKSUM_CRC32 if crc else O.CHKSUM_NONE
         self.w8 = FIELD_BITS[ec_type] == 8
         if self.w8:
             self.kind = O.ISAL_CAUCHY if ec_type == "isa_l_rs_cauchy" else O.ISAL_VAND
@@ -158,10 +162,10 @@ class OracleCodec:
         O, L = self.O, self.L
         t0 = time.perf_counter()
         if self.w8:
-            rc = L.o8_encode(self.kind, self.k, self.m, O.CHKSUM_NONE, O.LIBEC_VERSION,
+            rc = L.o8_encode(self.kind, self.k, self.m, self.ct, O.LIBEC_VERSION,
                              self.obj.ctypes.data, self.n, self.frags.ctypes.data)
         else:
-            rc = L.orc_encode(self.k, self.m, O.CHKSUM_NONE, O.LIBEC_VERSION,
+            rc = L.orc_encode(self.k, self.m, self.ct, O.LIBEC_VERSION,
                               self.obj.ctypes.data, self.n, self.frags.ctypes.data)
         dt = time.perf_counter() - t0
         assert rc == 0, f"oracle encode rc={rc}"
@@ -191,10 +195,10 @@ class OracleCodec:
         O = self.O
         t0 = time.perf_counter()
         if self.w8:
-            rc = self.L.o8_reconstruct(self.kind, self.k, self.m, O.CHKSUM_NONE, O.LIBEC_VERSION,
+            rc = self.L.o8_reconstruct(self.kind, self.k, self.m, self.ct, O.LIBEC_VERSION,
                                        arr, cnt, self.fl, dest, self.rec.ctypes.data)
         else:
-            rc = self.L.orc_reconstruct(self.k, self.m, O.CHKSUM_NONE, O.LIBEC_VERSION, arr,
+            rc = self.L.orc_reconstruct(self.k, self.m, self.ct, O.LIBEC_VERSION, arr,
                                         cnt, self.fl, dest, self.rec.ctypes.data)
         dt = time.perf_counter() - t0
         assert rc == 0, f"oracle reconstruct rc={rc}"
@@ -206,7 +210,7 @@ def oracle_pass(args, host, masks, dests, gpu_frags=None, gpu_second=None, sampl
     outputs are given -- compare every fragment (header included) and every
     decoded object / rebuilt fragment with it.  Returns (t_enc, t_two, bad)."""
     k, m, n = args.k, args.m, args.obj_bytes
-    oc = OracleCodec(args.ec_type, k, m, n)
+    oc = OracleCodec(args.ec_type, k, m, n, crc=getattr(args, "inline_crc32", False))
     fl = oc.fl
     t_enc = t_two = 0.0
     bad = []
@@ -234,7 +238,7 @@ def _cpu_worker(path, shape, lo, hi, args_dict, masks, dests, barrier, q):
     with the scalar oracle, after every worker is ready."""
     host = np.memmap(path, dtype=np.uint8, mode="r", shape=shape)
     a = argparse.Namespace(**args_dict)
-    oc = OracleCodec(a.ec_type, a.k, a.m, a.obj_bytes)
+    oc = OracleCodec(a.ec_type, a.k, a.m, a.obj_bytes, crc=getattr(a, "inline_crc32", False))
     np.asarray(host[lo:hi]).sum()  # page the slice in before the clock starts
     barrier.wait()
     t0 = time.perf_counter()
@@ -264,8 +268,8 @@ def cpu_parallel(args, host, masks, dests, sample, workers):
         del mm
         ctx = mp.get_context("spawn")
         barrier, q = ctx.Barrier(workers), ctx.Queue()
-        keys = ("ec_type", "k", "m", "obj_bytes", "second")
-        ad = {key: getattr(args, key) for key in keys}
+        keys = ("ec_type", "k", "m", "obj_bytes", "second", "inline_crc32")
+        ad = {key: getattr(args, key, False) for key in keys}
         for w in range(workers):
             lo, hi = sample * w // workers, sample * (w + 1) // workers
             p = ctx.Process(target=_cpu_worker,
@@ -488,7 +492,7 @@ def main():
     two = args.second
     two_masks = masks if two == "decode" else rmasks
 
-    codec = batch.BatchCodec(k, m, ec_type=args.ec_type)
+    codec = batch.BatchCodec(k, m, ec_type=args.ec_type, inline_crc32=args.inline_crc32)
     objs = torch.from_numpy(host).to(dev)
     stripes = batch.stripe_buffer(B, k, m, bs, device=dev)
     out = torch.zeros((B, obj_stride), dtype=torch.uint8, device=dev)
@@ -554,7 +558,7 @@ def main():
     dom = two if dec_ms >= enc_ms else "encode"
     default_workload = (args.ec_type in ("amd_rs_vand", "liberasurecode_rs_vand") and k == 10
                         and m == 4 and n == 4 * 1024 * 1024 and two == "decode"
-                        and B == 256)
+                        and B == 256 and not args.inline_crc32)
     pmc = (load_pmc(os.path.join(ROOT, "profiles", "pmc_summary.json")) or {}) \
         if default_workload else {}
     lib_id = _native.build_id()
@@ -571,7 +575,8 @@ def main():
                 "library_id": lib_id}
 
     metric = METRIC if default_workload else (
-        f"device-resident encode+{two} GiB/s, {args.ec_type} k={k} m={m}, {n} B objects")
+        f"device-resident encode+{two} GiB/s, {args.ec_type} k={k} m={m}, {n} B objects"
+        + (", inline_crc32" if args.inline_crc32 else ""))
     result = {
         "metric": metric,
         "value": round(value, 3),

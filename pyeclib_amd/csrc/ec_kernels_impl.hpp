@@ -690,11 +690,15 @@ __global__ void __launch_bounds__(kThreadsPerBlock) copy_data_kernel(EncodeParam
 //
 // Object stores.  Decode writes data slice j of an object at j*bs + t, and
 // bs is rarely a multiple of 16 (419,432 = 8 mod 16 at 4 MiB, k = 10), so
-// lane stores straddle 16-B units.  Realigning them was measured three ways
+// lane stores straddle 16-B units.  Realigning them was measured four ways
 // and each lost to the plain stores (round 1-2, profiles/): an overlap lane
 // per chunk (1008-B chunks: +12 % HBM traffic), LDS-staged whole tiles (438
-// vs 444 us, and 3 waves per SIMD), and DPP-shifted units with half-unit
-// stores at the chunk ends (440.8 vs 436.6 us with the streaming kernel).
+// vs 444 us, and 3 waves per SIMD), DPP-shifted units with half-unit stores
+// at the chunk ends (440.8 vs 436.6 us with the streaming kernel), and
+// copies of misaligned present slices from a second load shifted by the
+// misalignment, so every copy store is a whole aligned unit (432.2 vs 417.8
+// us with the fused-edge kernel, profiles/r02o_ab_shift.txt: the extra load
+// per input and the 102-VGPR budget cost more than the alignment gains).
 
 struct Slots {
   uint32_t table;  // set in the current slot (0xFFFFFFFF = none)
@@ -1194,11 +1198,14 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
     if (!env_flag("ECAMD_EDGE_SIDE", false)) {
       p.fused_edges = 1;
       const uint32_t items = std::max(p.n_obj * p.tiles, edge_items);
-      if constexpr (K == 10 && MODE == kDecode)
+      int per_cu = kDecodePerCu;
+      if constexpr (K == 10 && MODE == kDecode) {
+        per_cu = env_int("ECAMD_DEC_PER_CU", kDecodePerCu);  // A/B
         if (probe)
-          return launch(decode_kernel<F, K, MODE, true>, p, lds, items, stream, kDecodePerCu,
+          return launch(decode_kernel<F, K, MODE, true>, p, lds, items, stream, per_cu,
                         kDecodeXcd);
-      return launch(decode_kernel<F, K, MODE>, p, lds, items, stream, kDecodePerCu, kDecodeXcd);
+      }
+      return launch(decode_kernel<F, K, MODE>, p, lds, items, stream, per_cu, kDecodeXcd);
     }
     p.fused_edges = 0;
     return fork_join(
