@@ -157,4 +157,20 @@ void build_crc_tables(uint32_t bs, uint32_t steps, CrcTables* out) {
   out->init_term = apply(zeros(bs), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
 }
 
+void build_crc_finish_tables(uint32_t bs, uint32_t tiles_total, CrcFinishTables* out) {
+  const Tables& tb = tables();
+  std::memset(out, 0, sizeof(*out));
+  Mat z = zeros(4096);
+  for (int i = 0; i < kCrcPowBits; ++i) {
+    nibble_tables(z, out->pow[i]);
+    z = compose(z, z);
+  }
+  Mat inv;
+  const uint64_t pad = uint64_t(tiles_total) * 4096 - bs;
+  if (!inverse(zeros(pad), inv)) inv = identity();  // Z_n is always invertible
+  nibble_tables(inv, out->unshift);
+  for (int i = 0; i < 256; ++i) out->t0[i] = tb.t[0][i];
+  out->init_term = apply(zeros(bs), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+}
+
 }  // namespace ecamd

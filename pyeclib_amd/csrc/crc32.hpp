@@ -41,4 +41,20 @@ static_assert(sizeof(CrcTables) % 16 == 0, "CrcTables is copied to LDS in 16-B p
 // Tables for payloads of `bs` bytes processed in `steps` rounds of 4 KiB.
 void build_crc_tables(uint32_t bs, uint32_t steps, CrcTables* out);
 
+// The encode kernel's fused parity CRC (ec_kernels_impl.hpp) leaves one raw
+// CRC per run of 4 KiB tiles; the finishing pass (ec_crc.hip) shifts each to
+// the end of the zero-padded payload, XORs them, removes the padding and
+// folds in the init / final XORs.
+constexpr int kCrcPowBits = 20;  // tiles_total < 2^20 (payloads < 4 GiB)
+struct CrcFinishTables {
+  uint32_t pow[kCrcPowBits][8][16];  // Z_{4096 * 2^i}
+  uint32_t unshift[8][16];           // Z_pad^-1, pad = tiles_total * 4096 - bs
+  uint32_t t0[256];                  // bytewise table (header metadata CRC)
+  uint32_t init_term;                // Z_bs(0xFFFFFFFF) ^ 0xFFFFFFFF
+  uint32_t pad[3];
+};
+static_assert(sizeof(CrcFinishTables) % 16 == 0, "copied to LDS in 16-B pieces");
+
+void build_crc_finish_tables(uint32_t bs, uint32_t tiles_total, CrcFinishTables* out);
+
 }  // namespace ecamd

@@ -16,12 +16,15 @@
 #include <cstddef>
 
 #include "crc32.hpp"
+#include "crc_device.hpp"
 #include "ec_crc.hpp"
 
 namespace ecamd {
 namespace {
 
-typedef __attribute__((address_space(3))) char lds_char;
+using crcdev::lds32;
+using crcdev::zmap;
+
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t kRaw16 = offsetof(CrcTables, raw16);
@@ -31,38 +34,7 @@ constexpr uint32_t kUnshift = offsetof(CrcTables, unshift);
 constexpr uint32_t kT0 = offsetof(CrcTables, t0);
 constexpr uint32_t kInit = offsetof(CrcTables, init_term);
 
-__device__ __forceinline__ uint32_t lds32(uint32_t byte) {
-  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(
-      reinterpret_cast<const lds_char*>(static_cast<uintptr_t>(byte)));
-}
-
-__device__ __forceinline__ uint32_t byte_of(uint32_t x, int b) { return (x >> (8 * b)) & 0xFFu; }
-
-// XOR over the 8 nibbles of r of the map's table [q][v] at LDS byte `tab`.
-__device__ __forceinline__ uint32_t zmap(uint32_t r, uint32_t tab) {
-  const uint32_t lo = (r << 2) & 0x3C3C3C3Cu, hi = (r >> 2) & 0x3C3C3C3Cu;
-  uint32_t a = 0;
-#pragma unroll
-  for (int b = 0; b < 4; ++b)
-    a ^= lds32(tab + 128 * b + byte_of(lo, b)) ^ lds32(tab + 128 * b + 64 + byte_of(hi, b));
-  return a;
-}
-
-// Raw CRC of one 16-byte chunk (32 nibble lookups).
-__device__ __forceinline__ uint32_t raw16(const uint4& x) {
-  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-  uint32_t a = 0;
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const uint32_t lo = (w[d] << 2) & 0x3C3C3C3Cu, hi = (w[d] >> 2) & 0x3C3C3C3Cu;
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const uint32_t p = 8 * d + 2 * b;  // nibble position of the byte's low nibble
-      a ^= lds32(kRaw16 + 64 * p + byte_of(lo, b)) ^ lds32(kRaw16 + 64 * (p + 1) + byte_of(hi, b));
-    }
-  }
-  return a;
-}
+__device__ __forceinline__ uint32_t raw16(const uint4& x) { return crcdev::raw16(x, kRaw16); }
 
 constexpr int kAhead = 4;
 
@@ -123,32 +95,117 @@ __global__ void __launch_bounds__(256) crc_kernel(CrcParams p) {
       const uint32_t a = zmap(partial[0], kLevel + 512 * 6) ^ partial[1];
       const uint32_t b = zmap(partial[2], kLevel + 512 * 6) ^ partial[3];
       const uint32_t raw = zmap(zmap(a, kLevel + 512 * 7) ^ b, kUnshift);
-      const uint32_t crc = raw ^ lds32(kInit);
-      // header bytes 0..63: patch chksum[0] (offset 21), then the metadata
-      // checksum over bytes 0..58 (offset 67)
-      uint32_t h[16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = reinterpret_cast<const uint4*>(frag)[q];
-        h[4 * q] = v.x;
-        h[4 * q + 1] = v.y;
-        h[4 * q + 2] = v.z;
-        h[4 * q + 3] = v.w;
-      }
-      // chksum occupies bytes 21..24: byte 21..23 in h[5] (bits 8..31), 24 in h[6]
-      h[5] = (h[5] & 0x000000FFu) | (crc << 8);
-      h[6] = (h[6] & 0xFFFFFF00u) | (crc >> 24);
-      uint32_t m = 0xFFFFFFFFu;
-      for (int b = 0; b < 59; ++b) m = lds32(kT0 + 4 * ((m ^ byte_of(h[b >> 2], b & 3)) & 0xFF)) ^ (m >> 8);
-      m ^= 0xFFFFFFFFu;
-      for (int b = 21; b < 25; ++b) frag[b] = static_cast<uint8_t>(crc >> (8 * (b - 21)));
-      for (int b = 67; b < 71; ++b) frag[b] = static_cast<uint8_t>(m >> (8 * (b - 67)));
+      crcdev::patch_header(frag, raw ^ lds32(kInit), kT0);
     }
     __syncthreads();  // partial[] is reused by the next fragment
   }
 }
 
+// LDS of the finishing pass: the CrcTables maps (raw16, z4096, level) at 0,
+// then the CrcFinishTables.
+constexpr uint32_t kFMaps = offsetof(CrcTables, unshift);
+constexpr uint32_t kFPow = kFMaps + offsetof(CrcFinishTables, pow);
+constexpr uint32_t kFUnshift = kFMaps + offsetof(CrcFinishTables, unshift);
+constexpr uint32_t kFT0 = kFMaps + offsetof(CrcFinishTables, t0);
+constexpr uint32_t kFInit = kFMaps + offsetof(CrcFinishTables, init_term);
+constexpr uint32_t kFRed = kFMaps + sizeof(CrcFinishTables);  // 4 wave partials
+constexpr uint32_t kFLds = kFRed + 16;
+
+// Z_{4096 * d}(r) by the binary expansion of d.
+__device__ __forceinline__ uint32_t shift_tiles(uint32_t r, uint32_t d) {
+  for (int i = 0; d != 0 && i < kCrcPowBits; ++i, d >>= 1)
+    if (d & 1u) r = zmap(r, kFPow + 512u * i);
+  return r;
+}
+
+// First interior item of block b of the encode launch (encode_crc_interior).
+__device__ __forceinline__ uint64_t run_begin(uint64_t n, uint32_t b, uint32_t g) {
+  return n * b / g;
+}
+
+// One block per parity fragment (object o, row row0 + f % nrows).
+__global__ void __launch_bounds__(256) crc_finish_kernel(CrcFinishParams p) {
+  {
+    auto* dst = reinterpret_cast<__attribute__((address_space(3))) v4u*>(static_cast<uintptr_t>(0));
+    const v4u* maps = reinterpret_cast<const v4u*>(p.maps);
+    for (uint32_t i = threadIdx.x; i < kFMaps / 16; i += blockDim.x) dst[i] = maps[i];
+    const v4u* fin = reinterpret_cast<const v4u*>(p.tables);
+    for (uint32_t i = threadIdx.x; i < sizeof(CrcFinishTables) / 16; i += blockDim.x)
+      dst[kFMaps / 16 + i] = fin[i];
+  }
+  __syncthreads();
+  auto* red = reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+      static_cast<uintptr_t>(kFRed));
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t total = p.tiles + p.edge_tiles;
+  for (uint32_t f = blockIdx.x; f < p.n_obj * p.nrows; f += gridDim.x) {
+    const uint32_t o = f / p.nrows, row = p.row0 + (f - o * p.nrows);
+    uint8_t* frag = p.parity + static_cast<uint64_t>(o) * p.stripe_stride + row * p.frag_stride;
+    // edge tiles: their raw CRC from the payload (bytes past bs count as zero)
+    uint32_t edge = 0;
+    for (uint32_t e = 0; e < p.edge_tiles; ++e) {
+      const uint32_t off = (p.tiles + e) * 4096 + threadIdx.x * 16;
+      uint4 x = make_uint4(0, 0, 0, 0);
+      if (off < p.bs) {  // off + 16 <= round16(bs): inside the fragment slot
+        const v4u v = *reinterpret_cast<const v4u*>(frag + 80 + off);
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        const int64_t rem = static_cast<int64_t>(p.bs) - off;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t valid = rem - 4 * i;
+          w[i] &= valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : (1u << (8 * valid)) - 1u);
+        }
+        x = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+      uint32_t acc = crcdev::raw16(x, 0);
+#pragma unroll
+      for (int l = 0; l < 6; ++l) {
+        const uint32_t other = __shfl_down(acc, 1u << l, 64);
+        acc = zmap(acc, kLevel + 512 * l) ^ other;
+      }
+      if (lane == 0) red[wave] = acc;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const uint32_t a = zmap(red[0], kLevel + 512 * 6) ^ red[1];
+        const uint32_t b = zmap(red[2], kLevel + 512 * 6) ^ red[3];
+        edge ^= shift_tiles(zmap(a, kLevel + 512 * 7) ^ b, p.edge_tiles - 1 - e);
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x != 0) continue;
+    const uint32_t* part = p.part + static_cast<uint64_t>(o) * total * p.m + row;
+    uint32_t acc = edge;
+    if (p.tiles != 0) {
+      // the runs of object o's interior tiles: cut at the launch's block ranges
+      const uint64_t n = static_cast<uint64_t>(p.n_obj) * p.tiles;
+      const uint64_t lo = static_cast<uint64_t>(o) * p.tiles, hi = lo + p.tiles;
+      uint32_t b = static_cast<uint32_t>(lo * p.grid / n);
+      while (b > 0 && run_begin(n, b, p.grid) > lo) --b;
+      while (b + 1 < p.grid && run_begin(n, b + 1, p.grid) <= lo) ++b;
+      for (uint64_t s = lo; s < hi; ++b) {
+        const uint64_t e = std::min<uint64_t>(b + 1 < p.grid ? run_begin(n, b + 1, p.grid) : n, hi);
+        if (e <= s) continue;  // empty block range
+        const uint32_t t0 = static_cast<uint32_t>(s - lo), t1 = static_cast<uint32_t>(e - lo);
+        acc ^= shift_tiles(part[static_cast<uint64_t>(t0) * p.m], total - t1);
+        s = e;
+      }
+    }
+    crcdev::patch_header(frag, zmap(acc, kFUnshift) ^ lds32(kFInit), kFT0);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_crc_finish(const CrcFinishParams& p, hipStream_t stream) {
+  const uint32_t total = p.n_obj * p.nrows;
+  if (total == 0) return hipSuccess;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint32_t grid = std::min<uint32_t>(total, static_cast<uint32_t>(cus) * 4);
+  hipLaunchKernelGGL(crc_finish_kernel, dim3(grid), dim3(256), kFLds, stream, p);
+  return hipGetLastError();
+}
 
 hipError_t launch_crc(const CrcParams& p, hipStream_t stream) {
   const uint32_t total = p.n_obj * p.count;

@@ -63,6 +63,13 @@ struct EncodeParams {
   uint32_t tiles, edge_tiles;  // set by the launcher: interior / edge items per object
   uint32_t xcd_split;          // set by the launcher (item_range)
   uint32_t fused_edges;        // set by the launcher: edge items run in the interior launch
+  // inline_crc32 fused into the encode (null: no parity CRC in this launch):
+  // CrcTables (its raw16 / z4096 / level maps), CrcFinishTables for
+  // (bs, ceil(bs / 4096)), and n_obj * ceil(bs / 4096) * m u32 of run
+  // partials (ec_crc.hpp CrcFinishParams)
+  const void* crc_tables;
+  const void* crc_finish_tables;
+  uint32_t* crc_part;
 };
 
 // Per-object decode / reconstruct descriptor (device memory).

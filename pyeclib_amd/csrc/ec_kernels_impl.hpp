@@ -45,6 +45,9 @@
 #include <mutex>
 #include <unordered_map>
 
+#include "crc32.hpp"
+#include "crc_device.hpp"
+#include "ec_crc.hpp"
 #include "ec_kernels.hpp"
 
 namespace ecamd {
@@ -508,10 +511,13 @@ __host__ __device__ constexpr int stream_bufs() {
 
 // Waves per SIMD the streaming kernels are built for (register budget) and
 // launched at (blocks per CU; each block has one wave per SIMD).  Decode runs
-// fewer blocks than its budget allows: 4 per CU measured best at k = 10
-// (436.6 us vs 450.5 at 6 and 475.2 at 8).
+// fewer blocks than its budget allows: with the edges fused into the launch,
+// 2 per CU measured best at k = 10 (same process, profiles/r02q_ab_per_cu.txt,
+// r02r_ab_per_cu.txt: 405.8 us at 2, 411.8 at 3, 424.1 at 4, 424.5 at 5);
+// encode keeps 8 (302.1 us vs 302.9 at 6, 304.4 at 7).
 constexpr int kEncodeOcc = 8, kEncodePerCu = 8;
-constexpr int kDecodeOcc = 6, kDecodePerCu = 4;
+constexpr int kEncodeCrcOcc = 5;  // the fused-CRC encode's register budget (96 VGPRs)
+constexpr int kDecodeOcc = 6, kDecodePerCu = 2;
 // Decode walks its items without the XCD-major split (grid-stride over the
 // whole list): measured round 2, same process, three boxes: 437.0 vs 446.1,
 // 438.8 vs 445.6, 436.5 vs 444.3 us.  Encode is indifferent (+-0.3 us) and
@@ -656,6 +662,145 @@ __global__ void __launch_bounds__(kThreadsPerBlock) encode_edge_kernel(EncodePar
   load_tables(p.tables, K * F::kTableBytes, 0);
   __syncthreads();
   encode_edges<F, K, NR>(p, blockIdx.x, gridDim.x);
+}
+
+// ---------------- encode with the parity CRC fused (inline_crc32) ----------------
+//
+// liberasurecode's set_checksum (upstream erasurecode_helpers.c; pyeclib
+// core.py:59-63 -> pyeclib_c.c:248) writes zlib crc32(0, payload, bs) into
+// every fragment header.  A separate CRC pass re-reads every parity payload
+// and is lookup-bound (measured round 2: +136 us on the 310-us encode at
+// 256 x 4 MiB, profiles/r02p); here the encode kernel takes the raw CRC of
+// the parity chunks it has just computed, in registers.
+//
+// The raw CRC is GF(2)-linear: raw(A || B) = Z_|B|(raw(A)) ^ raw(B).  Each
+// block walks a CONTIGUOUS range of interior items (not grid-stride), so a
+// thread's consecutive pieces of one parity payload are 4 KiB apart and it
+// keeps their raw CRC in Horner form acc = Z_4096(acc) ^ raw16(piece) (40
+// nibble lookups per 16 B and row).  When the range leaves an object (or
+// ends), the block joins its 256 threads with the lane tree of the CRC pass
+// and stores one raw CRC per row for that run.  crc_finish_kernel (one block
+// per parity fragment) takes the edge tiles' raw CRC from the payload just
+// written, shifts every run to the end of the payload and finishes the
+// header.  Data fragments, when materialised, keep the CRC pass.
+
+constexpr uint32_t kCrcLdsBytes = offsetof(CrcTables, unshift);  // raw16, z4096, level[8]
+constexpr uint32_t kCrcZ4096 = offsetof(CrcTables, z4096);
+constexpr uint32_t kCrcLevel = offsetof(CrcTables, level);
+template <class F, int K>
+__host__ __device__ constexpr uint32_t crc_lds_base() {
+  return (K * F::kTableBytes + 255u) & ~255u;
+}
+template <class F, int K>
+__host__ __device__ constexpr uint32_t crc_lds_bytes() {
+  return crc_lds_base<F, K>() + kCrcLdsBytes + 4 * kWavesPerBlock * 4;  // + run partials
+}
+
+// Join the block's 256 per-thread raw CRCs of NR rows (thread t's pieces at
+// 16 t within each tile) and store row q's at dst[q]; zeroes acc.  Block-uniform.
+template <int NR>
+__device__ __forceinline__ void crc_block_flush(uint32_t (&acc)[NR], uint32_t base, uint32_t* dst) {
+  const uint32_t lane = lane_id(), wave = wave_in_block();
+  const uint32_t lev = base + kCrcLevel, red = base + kCrcLdsBytes;
+#pragma unroll
+  for (int q = 0; q < NR; ++q) {
+    uint32_t a = acc[q];
+#pragma unroll
+    for (int l = 0; l < 6; ++l) {
+      const uint32_t other = __shfl_down(a, 1u << l, 64);
+      a = crcdev::zmap(a, lev + 512u * l) ^ other;
+    }
+    if (lane == 0)
+      *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+          static_cast<uintptr_t>(red + 4 * (wave * NR + q))) = a;
+    acc[q] = 0;
+  }
+  __syncthreads();
+  if (threadIdx.x < static_cast<uint32_t>(NR)) {
+    const uint32_t q = threadIdx.x;
+    const uint32_t p0 = crcdev::lds32(red + 4 * q), p1 = crcdev::lds32(red + 4 * (NR + q));
+    const uint32_t p2 = crcdev::lds32(red + 4 * (2 * NR + q)), p3 = crcdev::lds32(red + 4 * (3 * NR + q));
+    const uint32_t a = crcdev::zmap(p0, lev + 512u * 6) ^ p1;
+    const uint32_t b = crcdev::zmap(p2, lev + 512u * 6) ^ p3;
+    dst[q] = crcdev::zmap(a, lev + 512u * 7) ^ b;
+  }
+  __syncthreads();
+}
+
+// Run partials of object o from tile `tile` on, rows row0.. (ec_crc.hpp layout).
+__device__ __forceinline__ uint32_t* crc_part_at(const EncodeParams& p, uint32_t o, uint32_t tile) {
+  return p.crc_part + (static_cast<uint64_t>(o) * (p.tiles + p.edge_tiles) + tile) * p.m + p.row0;
+}
+
+// Interior with the parity CRC: block b streams the contiguous items
+// [n*b/G, n*(b+1)/G) (ec_crc.hip run_begin), otherwise as encode_interior.
+template <class F, int K, int NR>
+__device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
+  constexpr int NB = stream_bufs<K>();
+  constexpr uint32_t base = crc_lds_base<F, K>();
+  const uint64_t n = static_cast<uint64_t>(p.n_obj) * p.tiles;
+  const uint32_t begin = static_cast<uint32_t>(n * blockIdx.x / gridDim.x);
+  const uint32_t end = static_cast<uint32_t>(n * (blockIdx.x + 1) / gridDim.x);
+  uint32_t w = begin;
+  if (w >= end) return;
+  uint32_t o, x;
+  enc_item_pos(p, w, o, x);
+  uint32_t run0 = w - o * p.tiles;  // first tile of the current run
+  Rsrc cur = rsrc(p.objs + static_cast<uint64_t>(o) * p.obj_stride);
+  const uint32_t lane16 = lane_id() * 16;
+  uint4 buf[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) buf[j] = buf_ld<true>(cur, lane16, j * p.bs + x);
+  uint32_t acc[NR];
+#pragma unroll
+  for (int q = 0; q < NR; ++q) acc[q] = 0;
+  while (true) {
+    const uint32_t wn = w + 1 < end ? w + 1 : w;
+    uint32_t on, xn;
+    enc_item_pos(p, wn, on, xn);
+    const Rsrc nxt = rsrc(p.objs + static_cast<uint64_t>(on) * p.obj_stride, wn == w ? 0 : -1);
+    typename F::Acc s;
+    F::zero(s);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[j % NB], s);
+      if (j + NB < K)
+        buf[j % NB] = buf_ld<true>(cur, lane16, (j + NB) * p.bs + x);
+      else
+        buf[j % NB] = buf_ld<true>(nxt, lane16, (j + NB - K) * p.bs + xn);
+    }
+    F::pin(s);
+    const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
+    const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      const uint4 v = F::row(s, q);
+      buf_st(par, lane16, soff + q * p.frag_stride, v);
+      acc[q] = crcdev::zmap(acc[q], base + kCrcZ4096) ^ crcdev::raw16(v, base);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (wn == w || on != o) {  // the run ends: object boundary or the block's last item
+      crc_block_flush<NR>(acc, base, crc_part_at(p, o, run0));
+      run0 = 0;
+    }
+    if (wn == w) break;
+    w = wn;
+    o = on;
+    x = xn;
+    cur = nxt;
+  }
+}
+
+template <class F, int K, int NR>
+__global__ void __launch_bounds__(kThreadsPerBlock)
+    __attribute__((amdgpu_waves_per_eu(kEncodeCrcOcc, 8))) encode_crc_kernel(EncodeParams p) {
+  load_tables(p.tables, K * F::kTableBytes, 0);
+  load_tables(static_cast<const uint32_t*>(p.crc_tables), kCrcLdsBytes, crc_lds_base<F, K>());
+  __syncthreads();
+  // headers and edge items as encode_kernel; the edge tiles' CRC is taken by
+  // crc_finish_kernel from the parity just written
+  encode_edges<F, K, NR>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
+  encode_crc_interior<F, K, NR>(p);
 }
 
 // Data fragments (optional output of encode): the k padded object slices
@@ -1043,12 +1188,13 @@ inline bool lds_starts_at_zero(const void* kern) {
 
 template <typename Kern, typename Params>
 hipError_t launch(Kern kern, Params p, size_t lds, uint32_t items, hipStream_t stream,
-                  int max_per_cu = 4, bool xcd = true) {
+                  int max_per_cu = 4, bool xcd = true, int* grid_out = nullptr) {
   if (items == 0) return hipSuccess;
   const void* k = reinterpret_cast<const void*>(kern);
   if (!lds_starts_at_zero(k)) return hipErrorInvalidKernelFile;
   const int grid = grid_for(k, lds, items, max_per_cu);
   p.xcd_split = (grid >= 8 && grid % 8 == 0 && env_flag("ECAMD_XCD", xcd)) ? 1u : 0u;
+  if (grid_out) *grid_out = grid;
 
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreadsPerBlock), lds, stream, p);
   return hipGetLastError();
@@ -1127,6 +1273,35 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     per_cu = env_int("ECAMD_ENC_PER_CU", kEncodePerCu);  // A/B
   }
   hipError_t e;
+  if (p.crc_tables != nullptr) {
+    // inline_crc32 with the parity CRC fused: one encode launch + the
+    // finishing pass over the run partials
+    p.fused_edges = 1;
+    const uint32_t items = std::max({p.n_obj * p.tiles, p.n_obj * p.edge_tiles,
+                                     p.headers ? p.n_obj : 0u});
+    int grid = 0;
+    e = launch(encode_crc_kernel<F, K, NR>, p, crc_lds_bytes<F, K>(), items, stream,
+               kEncodePerCu, false, &grid);
+    if (e != hipSuccess) return e;
+    CrcFinishParams fp{};
+    fp.parity = p.parity;
+    fp.frag_stride = p.frag_stride;
+    fp.stripe_stride = p.stripe_stride;
+    fp.part = p.crc_part;
+    fp.maps = p.crc_tables;
+    fp.tables = p.crc_finish_tables;
+    fp.n_obj = p.n_obj;
+    fp.m = p.m;
+    fp.row0 = p.row0;
+    fp.nrows = NR;
+    fp.bs = p.bs;
+    fp.tiles = p.tiles;
+    fp.edge_tiles = p.edge_tiles;
+    fp.grid = static_cast<uint32_t>(grid);
+    if ((e = launch_crc_finish(fp, stream)) != hipSuccess) return e;
+    if (p.data == nullptr || p.row0 != 0) return hipSuccess;
+    return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + kTile - 1) / kTile), stream);
+  }
   if (!env_flag("ECAMD_EDGE_SIDE", false)) {
     // one launch: interior stream + edge items + headers
     p.fused_edges = 1;

@@ -281,6 +281,10 @@ struct Instance {
   DevBuf hbuf[kHostStreams];
   hipEvent_t hdone[kHostStreams] = {};
   std::map<uint64_t, DevBuf> crc_tables;  // payload size -> CrcTables (device)
+  std::map<uint64_t, DevBuf> crc_finish;  // payload size -> CrcFinishTables (device)
+  DevBuf crc_part;                        // fused parity CRC: run partials
+  hipStream_t crc_part_stream = nullptr;  // stream of the last launch using crc_part
+  bool crc_part_used = false;
 
   // bytes of one table set (k inputs x up to 4 rows)
   size_t table_bytes() const { return static_cast<size_t>(k) * table_bytes_per_input(code.w); }
@@ -312,6 +316,8 @@ struct Instance {
     pin.release();
     for (auto& b : hbuf) b.release();
     for (auto& kv : crc_tables) kv.second.release();
+    for (auto& kv : crc_finish) kv.second.release();
+    crc_part.release();
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -802,30 +808,50 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
   return e2 == hipSuccess ? 0 : hip_errno(e2);
 }
 
+// Device copy of per-payload-size CRC tables (a bounded cache: when full,
+// wait for its users, then drop it).  Returns null on failure (*err set).
+template <class T, class Build>
+const void* crc_table_cache(std::map<uint64_t, DevBuf>& cache, uint64_t bs, Build build,
+                            hipError_t* err) {
+  *err = hipSuccess;
+  auto it = cache.find(bs);
+  if (it == cache.end()) {
+    if (cache.size() >= 16) {
+      (void)hipDeviceSynchronize();
+      for (auto& kv : cache) kv.second.release();
+      cache.clear();
+    }
+    std::unique_ptr<T> host(new T);
+    build(host.get());
+    DevBuf buf;
+    hipError_t e = buf.ensure(sizeof(T));
+    if (e == hipSuccess) e = hipMemcpy(buf.p, host.get(), sizeof(T), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      buf.release();
+      *err = e;
+      return nullptr;
+    }
+    it = cache.emplace(bs, buf).first;
+  }
+  return it->second.p;
+}
+
+const void* crc_tables_for(Instance& I, uint64_t bs, hipError_t* err) {
+  const uint32_t steps = static_cast<uint32_t>((bs + 4095) / 4096);
+  return crc_table_cache<CrcTables>(
+      I.crc_tables, bs, [&](CrcTables* t) { build_crc_tables(static_cast<uint32_t>(bs), steps, t); },
+      err);
+}
+
 // Inline CRC-32 of `count` fragments per object (caller holds I.mu): payload
 // checksum and metadata checksum patched into headers already written.
 int run_crc(Instance& I, uint8_t* base, uint64_t frag_stride, uint64_t stripe_stride,
             uint32_t count, int n_obj, uint64_t bs, hipStream_t stream) {
   if (bs == 0 || n_obj == 0 || count == 0) return 0;
   const uint32_t steps = static_cast<uint32_t>((bs + 4095) / 4096);
-  auto it = I.crc_tables.find(bs);
-  if (it == I.crc_tables.end()) {
-    if (I.crc_tables.size() >= 16) {  // bounded cache: wait for users, then drop it
-      (void)hipDeviceSynchronize();
-      for (auto& kv : I.crc_tables) kv.second.release();
-      I.crc_tables.clear();
-    }
-    CrcTables host;
-    build_crc_tables(static_cast<uint32_t>(bs), steps, &host);
-    DevBuf buf;
-    hipError_t e = buf.ensure(sizeof(CrcTables));
-    if (e == hipSuccess) e = hipMemcpy(buf.p, &host, sizeof(CrcTables), hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-      buf.release();
-      return hip_errno(e);
-    }
-    it = I.crc_tables.emplace(bs, buf).first;
-  }
+  hipError_t te;
+  const void* tables = crc_tables_for(I, bs, &te);
+  if (!tables) return hip_errno(te);
   CrcParams P{};
   P.frags = base;
   P.frag_stride = frag_stride;
@@ -835,7 +861,7 @@ int run_crc(Instance& I, uint8_t* base, uint64_t frag_stride, uint64_t stripe_st
   P.n_obj = static_cast<uint32_t>(n_obj);
   P.bs = static_cast<uint32_t>(bs);
   P.steps = steps;
-  P.tables = it->second.p;
+  P.tables = tables;
   const hipError_t e = launch_crc(P, stream);
   return e == hipSuccess ? 0 : hip_errno(e);
 }
@@ -871,8 +897,43 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
                     &u);
     if (rc < 0) return rc;
   }
+  // inline_crc32: the parity CRC fused into the encode launch
+  // (ECAMD_CRC_FUSED=0: the separate CRC pass, as for data fragments)
+  const bool crc = headers && I.ct == CHKSUM_CRC32 && bs > 0;
+  const char* fused_env = std::getenv("ECAMD_CRC_FUSED");
+  const bool fused_crc = crc && !(fused_env && fused_env[0] == '0');
+  const void* crc_maps = nullptr;
+  const void* crc_fin = nullptr;
+  if (fused_crc) {
+    const uint32_t total = static_cast<uint32_t>((bs + 4095) / 4096);
+    hipError_t te;
+    if (!(crc_maps = crc_tables_for(I, bs, &te)) ||
+        !(crc_fin = crc_table_cache<CrcFinishTables>(
+              I.crc_finish, bs,
+              [&](CrcFinishTables* t) { build_crc_finish_tables(static_cast<uint32_t>(bs), total, t); },
+              &te))) {
+      (void)upload_done(I, u, stream);
+      return hip_errno(te);
+    }
+    // the partials buffer is reused call to call: a launch on another stream
+    // may still be reading it
+    if (I.crc_part_used && I.crc_part_stream != stream) (void)hipDeviceSynchronize();
+    const size_t part_bytes = static_cast<size_t>(n_obj) * total * m * sizeof(uint32_t);
+    if (part_bytes > I.crc_part.cap) {
+      if (I.crc_part_used) (void)hipDeviceSynchronize();
+      if ((e = I.crc_part.ensure(part_bytes)) != hipSuccess) {
+        (void)upload_done(I, u, stream);
+        return hip_errno(e);
+      }
+    }
+    I.crc_part_used = true;
+    I.crc_part_stream = stream;
+  }
   for (uint32_t p = 0; p < I.passes; ++p) {
     EncodeParams P{};
+    P.crc_tables = crc_maps;
+    P.crc_finish_tables = crc_fin;
+    P.crc_part = fused_crc ? static_cast<uint32_t*>(I.crc_part.p) : nullptr;
     P.objs = objs;
     P.obj_stride = obj_stride;
     P.obj_len = obj_len;
@@ -900,7 +961,7 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
   }
   if ((e = upload_done(I, u, stream)) != hipSuccess) return hip_errno(e);
   if (headers && I.ct == CHKSUM_CRC32) {
-    int rc = run_crc(I, parity, frag_stride, stripe_stride, m, n_obj, bs, stream);
+    int rc = fused_crc ? 0 : run_crc(I, parity, frag_stride, stripe_stride, m, n_obj, bs, stream);
     if (rc == 0 && data) rc = run_crc(I, data, frag_stride, stripe_stride, k, n_obj, bs, stream);
     if (rc < 0) return rc;
   }

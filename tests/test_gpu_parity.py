@@ -282,17 +282,21 @@ def test_isal_cauchy_batch(oracle, gpu, k, m, obj_len):
 
 # ---------------- inline CRC-32 on the batch path (GPU payload CRC kernel) ----------------
 
-@pytest.mark.parametrize("ec_type,k,m,obj_len", [
-    ("amd_rs_vand", 10, 4, 4 * 1024 * 1024), ("amd_rs_vand", 4, 2, 100001),
-    ("amd_rs_vand", 12, 2, 4096 * 12 * 2), ("amd_rs_vand", 3, 1, 17),
-    ("isa_l_rs_cauchy", 12, 4, 999999), ("isa_l_rs_vand", 8, 4, 65537)])
-def test_batch_inline_crc32(oracle, gpu, ec_type, k, m, obj_len):
+@pytest.mark.parametrize("ec_type,k,m,obj_len,n_obj", [
+    ("amd_rs_vand", 10, 4, 4 * 1024 * 1024, 3), ("amd_rs_vand", 4, 2, 100001, 3),
+    ("amd_rs_vand", 12, 2, 4096 * 12 * 2, 3), ("amd_rs_vand", 3, 1, 17, 3),
+    ("isa_l_rs_cauchy", 12, 4, 999999, 3), ("isa_l_rs_vand", 8, 4, 65537, 3),
+    # fused parity CRC: runs of many tiles cut at block and object boundaries
+    # (the grid is far smaller than the item list), multi-pass parity (m > 4)
+    ("amd_rs_vand", 10, 4, 4 * 1024 * 1024, 160), ("amd_rs_vand", 6, 6, 300000, 40),
+    ("isa_l_rs_cauchy", 12, 4, 3 * 1024 * 1024 + 5, 48)])
+def test_batch_inline_crc32(oracle, gpu, ec_type, k, m, obj_len, n_obj):
     """chksum_type inline_crc32 on device-resident batches: every header
     (payload CRC-32 + metadata checksum) equals the oracle's, for encode with
-    data fragments and for reconstruct."""
+    data fragments and for reconstruct.  The parity CRC is fused into the
+    encode launch; data fragments and reconstruct use the CRC pass."""
     import torch
     from pyeclib_amd import batch
-    n_obj = 3
     codec = batch.BatchCodec(k, m, inline_crc32=True, ec_type=ec_type)
     bs = codec.blocksize(obj_len)
     stride = (obj_len + 15) // 16 * 16
