@@ -518,6 +518,9 @@ __host__ __device__ constexpr int stream_bufs() {
 constexpr int kEncodeOcc = 8, kEncodePerCu = 8;
 constexpr int kEncodeCrcOcc = 5;  // the fused-CRC encode's register budget (96 VGPRs)
 constexpr int kDecodeOcc = 6, kDecodePerCu = 2;
+// Reconstruct (k reads, one row written) keeps 4 per CU: at 2 the config-3
+// reconstruct (GF(2^8), k = 12, 16 MiB) ran 0.586 ms vs 0.500 before.
+constexpr int kReconstructPerCu = 4;
 // Decode walks its items without the XCD-major split (grid-stride over the
 // whole list): measured round 2, same process, three boxes: 437.0 vs 446.1,
 // 438.8 vs 445.6, 436.5 vs 444.3 us.  Encode is indifferent (+-0.3 us) and
@@ -975,10 +978,10 @@ __device__ __forceinline__ Rsrc rsrc_out(const void* base) {
 // Stores that do not apply (parity inputs, rows past n_out) go to voffset
 // kDrop and are discarded by the range check, so every item issues the same
 // memory instructions.  NOCOMP: memory-only probe (no lookups; wrong rows).
-template <class F, int K, int MODE, bool NOCOMP = false>
+template <class F, int K, int MODE, bool NOCOMP = false, int NBX = 0>
 __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st,
                                                 TablePre<F, K>& pre) {
-  constexpr int NB = stream_bufs<K>();
+  constexpr int NB = NBX ? NBX : stream_bufs<K>();  // NBX: A/B (divides K)
   const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
   uint32_t w = r.begin;
   if (w >= r.end) return;  // block-uniform: no wave of this block reaches a barrier
@@ -1115,13 +1118,13 @@ __device__ __forceinline__ void decode_edges(const DecodeParams& p, uint32_t fir
 // counted from the end of the grid (see encode_kernel), then the interior
 // stream.  The interior's first table change goes into the LDS slot the edge
 // items did not use, behind a barrier, as between any two items.
-template <class F, int K, int MODE, bool NOCOMP = false>
+template <class F, int K, int MODE, bool NOCOMP = false, int NBX = 0>
 __global__ void __launch_bounds__(kThreadsPerBlock)
-    __attribute__((amdgpu_waves_per_eu(kDecodeOcc, 8))) decode_kernel(DecodeParams p) {
+    __attribute__((amdgpu_waves_per_eu(NBX > 6 ? 4 : kDecodeOcc, 8))) decode_kernel(DecodeParams p) {
   Slots st{0xFFFFFFFFu, 1u};
   TablePre<F, K> pre;
   if (p.fused_edges) decode_edges<F, K, MODE>(p, gridDim.x - 1 - blockIdx.x, gridDim.x, st, pre);
-  decode_interior<F, K, MODE, NOCOMP>(p, st, pre);
+  decode_interior<F, K, MODE, NOCOMP, NBX>(p, st, pre);
 }
 
 // The edge work in a launch of its own (side-stream variant, ECAMD_EDGE_SIDE=1).
@@ -1373,11 +1376,19 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
     if (!env_flag("ECAMD_EDGE_SIDE", false)) {
       p.fused_edges = 1;
       const uint32_t items = std::max(p.n_obj * p.tiles, edge_items);
-      int per_cu = kDecodePerCu;
+      int per_cu = MODE == kReconstruct ? env_int("ECAMD_REC_PER_CU", kReconstructPerCu)
+                                        : kDecodePerCu;
       if constexpr (K == 10 && MODE == kDecode) {
         per_cu = env_int("ECAMD_DEC_PER_CU", kDecodePerCu);  // A/B
         if (probe)
           return launch(decode_kernel<F, K, MODE, true>, p, lds, items, stream, per_cu,
+                        kDecodeXcd);
+        const int nb = env_int("ECAMD_DEC_NB", 0);  // A/B: inputs in flight per wave
+        if (nb == 10)
+          return launch(decode_kernel<F, K, MODE, false, 10>, p, lds, items, stream, per_cu,
+                        kDecodeXcd);
+        if (nb == 2)
+          return launch(decode_kernel<F, K, MODE, false, 2>, p, lds, items, stream, per_cu,
                         kDecodeXcd);
       }
       return launch(decode_kernel<F, K, MODE>, p, lds, items, stream, per_cu, kDecodeXcd);

@@ -34,6 +34,18 @@ for s in $STEPS; do
   timeline)
     python3 $R/tools/rocpd_timeline.py $O/prof --last 24 > $O/timeline.txt 2>&1 || true
     cat $O/timeline.txt ;;
+  config3)
+    (cd $R && timeout -k 10 400 python3 bench.py --ec-type isa_l_rs_cauchy --k 12 --m 4 \
+        --obj-bytes 16777216 --batch 128 --second reconstruct --steps 10 --no-host \
+        > $O/config3_bench.json 2> $O/config3_bench.err)
+    tail -c 700 $O/config3_bench.json ;;
+  swift)
+    (cd $R && timeout -k 10 400 python3 tools/swift_mix.py > $O/swift_mix.json 2> $O/swift_mix.err)
+    head -c 400 $O/swift_mix.json ;;
+  crc)
+    (cd $R && timeout -k 10 300 python3 bench.py --inline-crc32 --steps 10 --no-host \
+        --no-cpu-baseline > $O/bench_crc.json 2> $O/bench_crc.err)
+    tail -c 400 $O/bench_crc.json ;;
   bench)
     (cd $R && timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err)
     cat $O/bench.json ;;
