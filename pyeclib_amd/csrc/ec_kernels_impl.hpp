@@ -506,7 +506,15 @@ template <int K>
 __host__ __device__ constexpr int stream_bufs() {
   for (int d = 6; d >= 2; --d)
     if (K % d == 0) return d;
-  return K;
+  return K < 4 ? K : 4;  // prime K > 3: 4 buffers, the item padded (stream_slots)
+}
+// Slots per item: K rounded up to a multiple of NB.  Slots past K load and
+// compute nothing (compile-time), so every item still issues the same memory
+// instructions in the same order.  (Round 1-2 used NB = K for prime K: 7, 11,
+// 13, ... -- up to 31 inputs in registers, and the kernels spilled.)
+template <int K, int NB>
+__host__ __device__ constexpr int stream_slots() {
+  return (K + NB - 1) / NB * NB;
 }
 
 // Waves per SIMD the streaming kernels are built for (register budget) and
@@ -517,7 +525,7 @@ __host__ __device__ constexpr int stream_bufs() {
 // encode keeps 8 (302.1 us vs 302.9 at 6, 304.4 at 7).
 constexpr int kEncodeOcc = 8, kEncodePerCu = 8;
 constexpr int kEncodeCrcOcc = 5;  // the fused-CRC encode's register budget (96 VGPRs)
-constexpr int kDecodeOcc = 6, kDecodePerCu = 2;
+constexpr int kDecodeOcc = 4, kDecodePerCu = 2;
 // Reconstruct (k reads, one row written) keeps 4 per CU: at 2 the config-3
 // reconstruct (GF(2^8), k = 12, 16 MiB) ran 0.586 ms vs 0.500 before.
 constexpr int kReconstructPerCu = 4;
@@ -589,9 +597,11 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
   enc_item_pos(p, w, o, x);
   Rsrc cur = rsrc(p.objs + static_cast<uint64_t>(o) * p.obj_stride);
   const uint32_t lane16 = lane_id() * 16;
+  constexpr int KP = stream_slots<K, NB>();
   uint4 buf[NB];
 #pragma unroll
-  for (int j = 0; j < NB; ++j) buf[j] = buf_ld<true>(cur, lane16, j * p.bs + x);
+  for (int j = 0; j < NB; ++j)
+    if (j < K) buf[j] = buf_ld<true>(cur, lane16, j * p.bs + x);
   while (true) {
     // the next item, or this one again through a zero-record descriptor
     const uint32_t wn = w + r.step < r.end ? w + r.step : w;
@@ -601,20 +611,23 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
     typename F::Acc s;
     F::zero(s);
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      if constexpr (NOCOMP) {
-        uint32_t* a = reinterpret_cast<uint32_t*>(&s);
-        a[0] ^= buf[j % NB].x;
-        a[2] ^= buf[j % NB].y;
-        a[4] ^= buf[j % NB].z;
-        a[6] ^= buf[j % NB].w;
-      } else {
-        F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[j % NB], s);
+    for (int j = 0; j < KP; ++j) {
+      if (j < K) {
+        if constexpr (NOCOMP) {
+          uint32_t* a = reinterpret_cast<uint32_t*>(&s);
+          a[0] ^= buf[j % NB].x;
+          a[2] ^= buf[j % NB].y;
+          a[4] ^= buf[j % NB].z;
+          a[6] ^= buf[j % NB].w;
+        } else {
+          F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[j % NB], s);
+        }
       }
-      if (j + NB < K)
-        buf[j % NB] = buf_ld<true>(cur, lane16, (j + NB) * p.bs + x);
-      else
-        buf[j % NB] = buf_ld<true>(nxt, lane16, (j + NB - K) * p.bs + xn);
+      if (j + NB < KP) {
+        if (j + NB < K) buf[j % NB] = buf_ld<true>(cur, lane16, (j + NB) * p.bs + x);
+      } else if (j + NB - KP < K) {
+        buf[j % NB] = buf_ld<true>(nxt, lane16, (j + NB - KP) * p.bs + xn);
+      }
     }
     F::pin(s);
     const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
@@ -751,9 +764,11 @@ __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
   uint32_t run0 = w - o * p.tiles;  // first tile of the current run
   Rsrc cur = rsrc(p.objs + static_cast<uint64_t>(o) * p.obj_stride);
   const uint32_t lane16 = lane_id() * 16;
+  constexpr int KP = stream_slots<K, NB>();
   uint4 buf[NB];
 #pragma unroll
-  for (int j = 0; j < NB; ++j) buf[j] = buf_ld<true>(cur, lane16, j * p.bs + x);
+  for (int j = 0; j < NB; ++j)
+    if (j < K) buf[j] = buf_ld<true>(cur, lane16, j * p.bs + x);
   uint32_t acc[NR];
 #pragma unroll
   for (int q = 0; q < NR; ++q) acc[q] = 0;
@@ -765,12 +780,13 @@ __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
     typename F::Acc s;
     F::zero(s);
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[j % NB], s);
-      if (j + NB < K)
-        buf[j % NB] = buf_ld<true>(cur, lane16, (j + NB) * p.bs + x);
-      else
-        buf[j % NB] = buf_ld<true>(nxt, lane16, (j + NB - K) * p.bs + xn);
+    for (int j = 0; j < KP; ++j) {
+      if (j < K) F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[j % NB], s);
+      if (j + NB < KP) {
+        if (j + NB < K) buf[j % NB] = buf_ld<true>(cur, lane16, (j + NB) * p.bs + x);
+      } else if (j + NB - KP < K) {
+        buf[j % NB] = buf_ld<true>(nxt, lane16, (j + NB - KP) * p.bs + xn);
+      }
     }
     F::pin(s);
     const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
@@ -990,10 +1006,11 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
   dec_item_pos(p, w, o, x);
   DescU d = load_desc(p, o);
   Rsrc cur = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride);
+  constexpr int KP = stream_slots<K, NB>();
   uint4 buf[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j)
-    buf[j] = buf_ld(cur, lane16, in_pos(p, d, j) * p.frag_stride + kHeaderBytes + x);
+    if (j < K) buf[j] = buf_ld(cur, lane16, in_pos(p, d, j) * p.frag_stride + kHeaderBytes + x);
   table_prefetch<F, K>(p, d.table(), d.n_out() != 0, pre);
   while (true) {
     const uint32_t wn = w + r.step < r.end ? w + r.step : w;
@@ -1009,21 +1026,26 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
     typename F::Acc s;
     F::zero(s);
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      if constexpr (NOCOMP) {
-        uint32_t* a = reinterpret_cast<uint32_t*>(&s);
-        a[0] ^= buf[j % NB].x;
-      } else {
-        F::mac(kb, j * F::kTableBytes, buf[j % NB], s);
+    for (int j = 0; j < KP; ++j) {
+      if (j < K) {
+        if constexpr (NOCOMP) {
+          uint32_t* a = reinterpret_cast<uint32_t*>(&s);
+          a[0] ^= buf[j % NB].x;
+        } else {
+          F::mac(kb, j * F::kTableBytes, buf[j % NB], s);
+        }
+        if constexpr (MODE != kReconstruct)
+          buf_st(out, copy && d.in_idx(j) < static_cast<uint32_t>(K) ? lane16 : kDrop,
+                 d.in_idx(j) * p.bs + x, buf[j % NB]);
       }
-      if constexpr (MODE != kReconstruct)
-        buf_st(out, copy && d.in_idx(j) < static_cast<uint32_t>(K) ? lane16 : kDrop,
-               d.in_idx(j) * p.bs + x, buf[j % NB]);
-      if (j + NB < K)
-        buf[j % NB] = buf_ld(cur, lane16, in_pos(p, d, j + NB) * p.frag_stride + kHeaderBytes + x);
-      else
+      if (j + NB < KP) {
+        if (j + NB < K)
+          buf[j % NB] =
+              buf_ld(cur, lane16, in_pos(p, d, j + NB) * p.frag_stride + kHeaderBytes + x);
+      } else if (j + NB - KP < K) {
         buf[j % NB] =
-            buf_ld(nxt, lane16, in_pos(p, dn, j + NB - K) * p.frag_stride + kHeaderBytes + xn);
+            buf_ld(nxt, lane16, in_pos(p, dn, j + NB - KP) * p.frag_stride + kHeaderBytes + xn);
+      }
     }
     F::pin(s);
     if constexpr (MODE == kReconstruct) {

@@ -96,7 +96,10 @@ def _batch_layout(k, m, n_obj, obj_len):
 @pytest.mark.parametrize("k,m,obj_len", [(10, 4, 1 << 20), (10, 4, 4 * 1024 * 1024 // 7),
                                          (4, 2, 100001), (12, 4, 999999), (6, 9, 65538),
                                          (3, 1, 17), (10, 4, 10 * 4096 * 3),
-                                         (8, 3, 8 * 8192), (10, 4, 10 * 4096 + 2)])
+                                         (8, 3, 8 * 8192), (10, 4, 10 * 4096 + 2),
+                                         # prime k: padded stream slots (NB = 4)
+                                         (7, 3, 7 * 4096 * 5 + 13), (11, 4, 1 << 20),
+                                         (13, 3, (2 << 20) + 6)])
 def test_batch_encode_decode_reconstruct(oracle, gpu, k, m, obj_len):
     import torch
     from pyeclib_amd import batch
@@ -243,7 +246,8 @@ def test_isal_decode_reconstruct(amd, oracle, ec_type, kind, k, m):
 
 
 @pytest.mark.parametrize("k,m,obj_len", [(12, 4, 1 << 20), (12, 4, 999999), (10, 4, 65537),
-                                         (6, 2, 12 * 4096 * 3 + 5)])
+                                         (6, 2, 12 * 4096 * 3 + 5), (11, 3, (1 << 20) + 3),
+                                         (7, 4, 7 * 4096 * 9)])
 def test_isal_cauchy_batch(oracle, gpu, k, m, obj_len):
     """Device-resident batch API on the GF(2^8) Cauchy code (BASELINE config 4
     shape at a small batch): encode vs oracle, decode, reconstruct."""
