@@ -1306,7 +1306,7 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
                                      p.headers ? p.n_obj : 0u});
     int grid = 0;
     e = launch(encode_crc_kernel<F, K, NR>, p, crc_lds_bytes<F, K>(), items, stream,
-               kEncodePerCu, false, &grid);
+               env_int("ECAMD_CRC_PER_CU", kEncodePerCu), false, &grid);  // A/B knob
     if (e != hipSuccess) return e;
     CrcFinishParams fp{};
     fp.parity = p.parity;
