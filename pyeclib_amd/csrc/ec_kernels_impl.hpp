@@ -117,6 +117,9 @@ __device__ __forceinline__ uint4 buf_ld(Rsrc r, uint32_t voff, uint32_t soff) {
   const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, CACHED ? 0 : kNt);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// (Stores keep the nt policy.  Measured round 2 in the bench's alternating
+// encode/decode step, k = 10, 256 x 4 MiB, profiles/r02y_store_policy.txt:
+// nt 2,708 GiB/s; default policy 2,556; sc1 2,523; nt sc1 2,587.)
 // One wait state after a 16-B buffer store.  Measured on MI355X (round 2):
 // a `buffer_store_dwordx4 v[30:33], v52, s[24:27], s31 offen` directly
 // followed by a VALU write of v30 stored a wrong first dword.  hipcc's hazard
