@@ -126,12 +126,15 @@ def test_decode_pool_recycles_safely(gpu, oracle, monkeypatch):
                                            ("isa_l_rs_cauchy", 12, 4, 1 << 20),
                                            ("amd_rs_vand", 4, 2, 17)])
 @pytest.mark.parametrize("path", ["direct", "staged", "staged_out"])
+@pytest.mark.parametrize("crc", [False, True])
 def test_host_resident_encode_decode_reconstruct(gpu, oracle, monkeypatch, ec_type, k, m, n,
-                                                 path):
+                                                 path, crc):
     """ecamd_{encode,decode,reconstruct}_host_batch: pinned host in and out,
     against the oracle (encode, reconstruct) and the objects (decode).  Paths:
     kernels on the mapped host arrays (default), the copy-engine pipeline with
-    kernels writing host outputs, and the pipeline with D2H-staged outputs."""
+    kernels writing host outputs, and the pipeline with D2H-staged outputs.
+    crc: inline_crc32 headers (the parity CRC fused into the encode launch,
+    its finishing pass reading the payloads it wrote, wherever they are)."""
     import torch
     from pyeclib_amd import batch
     if path != "direct":
@@ -140,7 +143,8 @@ def test_host_resident_encode_decode_reconstruct(gpu, oracle, monkeypatch, ec_ty
         monkeypatch.setenv("ECAMD_HOST_STAGED_OUT", "1")
     B = 13
     host, masks, dests = _inputs(B, n, k, m, m, 97 + n)
-    codec = batch.BatchCodec(k, m, ec_type=ec_type)
+    codec = batch.BatchCodec(k, m, ec_type=ec_type, inline_crc32=crc)
+    ct = oracle.CHKSUM_CRC32 if crc else oracle.CHKSUM_NONE
     bs = codec.blocksize(n)
     fs = batch.frag_stride(bs)
     fl = 80 + bs
@@ -151,9 +155,9 @@ def test_host_resident_encode_decode_reconstruct(gpu, oracle, monkeypatch, ec_ty
     for o in range(B):
         data = host[o, :n].tobytes()
         if codec.w == 8:
-            w = oracle.isal_encode(oracle.ISAL_CAUCHY, k, m, data)
+            w = oracle.isal_encode(oracle.ISAL_CAUCHY, k, m, data, ct=ct)
         else:
-            w = oracle.encode(k, m, data)
+            w = oracle.encode(k, m, data, ct=ct)
         want.append(w)
         for p in range(m):
             assert par[o, p, :fl].numpy().tobytes() == w[k + p], (o, p)
