@@ -62,7 +62,7 @@ FIELD_BITS = {"amd_rs_vand": 16, "liberasurecode_rs_vand": 16, "isa_l_rs_vand": 
               "isa_l_rs_cauchy": 8}
 SEED = 20261015
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-CPU_WORKERS_MAX = 16    # the GPU box's CPU share per GPU
+CPU_WORKERS_PER_GPU = 16  # the GPU box's CPU share per GPU
 
 
 def parse(argv=None):
@@ -92,6 +92,19 @@ def parse(argv=None):
     ap.add_argument("--no-host", action="store_true",
                     help="skip the host-resident (pinned H2D/D2H) encode/decode timing")
     ap.add_argument("--host", action="store_true", help=argparse.SUPPRESS)  # always on now
+    ap.add_argument("--fresh-steps", type=int, default=8,
+                    help="decode steps whose erasure masks are new every step (drawn from "
+                         "the seed outside the clock, handed over inside it): timed apart "
+                         "from the headline step, which replays one batch of masks")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (exercises the N-rank path on one GPU)")
+    ap.add_argument("--no-numa", action="store_true",
+                    help="do not bind each rank's CPUs to its GPU's NUMA node")
+    ap.add_argument("--cpu-baseline-all", action="store_true",
+                    help="also run the CPU baseline when N > 1 (default: N = 1 only)")
+    ap.add_argument("--config0", action="store_true",
+                    help="BASELINE configs[0]: time tools/pyeclib_encode.py / "
+                         "pyeclib_decode.py (k=4 m=2, one 1 MiB file) and the oracle")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch the ranks and the process group (gloo) without a GPU")
     return ap.parse_args(argv)
@@ -423,9 +436,12 @@ def single_object_calls(args, sizes=(64 << 10, 1 << 20, 4 << 20), reps=20):
             td.append(t2 - t1)
         oc = OracleCodec(args.ec_type, k, m, n)
         arr = np.frombuffer(data, dtype=np.uint8)
-        ce = [oc.encode(arr) for _ in range(3)]
         mask = ((1 << (k + m)) - 1) & ~((1 << lost) - 1)
-        cd = [oc.decode(mask) for _ in range(3)]
+        for _ in range(2):  # warm: page in the buffers and the tables
+            oc.encode(arr)
+            oc.decode(mask)
+        ce = [oc.encode(arr) for _ in range(reps)]
+        cd = [oc.decode(mask) for _ in range(reps)]
         res[f"{n >> 10}KiB"] = {
             "gpu_encode_us": round(1e6 * float(np.median(te)), 1),
             "gpu_decode_us": round(1e6 * float(np.median(td)), 1),
@@ -436,22 +452,145 @@ def single_object_calls(args, sizes=(64 << 10, 1 << 20, 4 << 20), reps=20):
     return {"single_object_calls": res,
             "single_object_note": f"ECDriver({k},{m},{ec_type}) per-call latency, pageable bytes "
                                   f"in/out, median of {reps}; decode with {min(args.erasures, m)} "
-                                  "data fragments missing; oracle = scalar C restatement, 1 core"}
+                                  "data fragments missing; oracle = scalar C restatement, 1 core, "
+                                  f"2 warm-up calls then the median of {reps}"}
 
 
 # ---------------- main ----------------
 
 def dry_run(args):
-    from pyeclib_amd import shard
-    world, rank, _ = shard.init("gloo")
+    from pyeclib_amd import placement, shard
+    world, rank, local = shard.init("gloo")
+    numa = placement.bind_to_gpu_numa(shard.device_index(local, args.same_device),
+                                      apply=False)
     t = shard.max_over_ranks(float(rank))
+    ok = shard.min_over_ranks(1)
     shard.barrier()
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "requested_gpus": args.gpus,
-                          "max_rank": t}), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+                          "max_rank": t, "all_ok": ok, "numa": numa}), flush=True)
+    shard.finish()
+
+
+# ---------------- configs[0]: the file CLI on k=4 m=2 ----------------
+
+def config0_cli(args, size=1 << 20, reps=5):
+    """BASELINE configs[0]: one 1 MiB file through tools/pyeclib_encode.py and
+    tools/pyeclib_decode.py (the reference's positional CLI,
+    tools/pyeclib_encode.py:27-37 there), k=4 m=2, GPU ec_type, with m random
+    fragments dropped before the decode (test/ec_pyeclib_file_test.sh's
+    recipe).  Reports the CLI wall time (a fresh interpreter per call, as a
+    user runs it) and the in-process ECDriver time for the same bytes, plus
+    the scalar oracle (1 core) on the same file."""
+    import random
+    import tempfile
+    from pyeclib_amd import ECDriver
+    k, m = 4, 2
+    ec_type = "liberasurecode_rs_vand"
+    rng = np.random.Generator(np.random.PCG64(SEED + 11))
+    data = rng.integers(0, 256, size=size, dtype=np.uint8).tobytes()
+    pick = random.Random(SEED)
+    out = {}
+    with tempfile.TemporaryDirectory(prefix="ecamd_cfg0_") as d:
+        src = os.path.join(d, "file.bin")
+        with open(src, "wb") as fh:
+            fh.write(data)
+        fdir = os.path.join(d, "frags")
+        os.makedirs(fdir)
+        enc = [sys.executable, os.path.join(ROOT, "tools", "pyeclib_encode.py"), str(k), str(m),
+               "0", ec_type, d, "file.bin", fdir]
+        t_enc, t_dec = [], []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            subprocess.run(enc, check=True, stdout=subprocess.DEVNULL)
+            t_enc.append(time.perf_counter() - t0)
+            keep = sorted(pick.sample(range(k + m), k))
+            dec = [sys.executable, os.path.join(ROOT, "tools", "pyeclib_decode.py"), str(k), str(m),
+                   "0", ec_type] + [os.path.join(fdir, f"file.bin.{i}") for i in keep] + \
+                  [os.path.join(d, "out")]
+            t0 = time.perf_counter()
+            subprocess.run(dec, check=True, stdout=subprocess.DEVNULL)
+            t_dec.append(time.perf_counter() - t0)
+            with open(os.path.join(d, "out.decoded"), "rb") as fh:
+                if fh.read() != data:
+                    raise SystemExit("configs[0]: decoded file differs from the input")
+    mib = size / 2**20
+    out["cli_encode_s"] = round(float(np.median(t_enc)), 4)
+    out["cli_decode_s"] = round(float(np.median(t_dec)), 4)
+    out["cli_encode_MiBps"] = round(mib / out["cli_encode_s"], 2)
+    out["cli_decode_MiBps"] = round(mib / out["cli_decode_s"], 2)
+    # in process: the ECDriver calls the CLI makes, without interpreter start-up
+    drv = ECDriver(k=k, m=m, ec_type=ec_type)
+    frags = drv.encode(data)
+    te, td = [], []
+    for _ in range(20):
+        t0 = time.perf_counter()
+        frags = drv.encode(data)
+        te.append(time.perf_counter() - t0)
+        keep = sorted(pick.sample(range(k + m), k))
+        t0 = time.perf_counter()
+        got = drv.decode([frags[i] for i in keep])
+        td.append(time.perf_counter() - t0)
+        if got != data:
+            raise SystemExit("configs[0]: in-process decode differs from the input")
+    drv.close()
+    out["inproc_encode_us"] = round(1e6 * float(np.median(te)), 1)
+    out["inproc_decode_us"] = round(1e6 * float(np.median(td)), 1)
+    out["inproc_encode_MiBps"] = round(mib / float(np.median(te)), 1)
+    out["inproc_decode_MiBps"] = round(mib / float(np.median(td)), 1)
+    # the scalar oracle on the same file (CPU baseline leg: 1 core)
+    oc = OracleCodec(ec_type, k, m, size)
+    arr = np.frombuffer(data, dtype=np.uint8)
+    mask = ((1 << (k + m)) - 1) & ~0b11  # data fragments 0 and 1 lost: the GF path
+    for _ in range(2):
+        oc.encode(arr)
+        oc.decode(mask)
+    ce = [oc.encode(arr) for _ in range(20)]
+    cd = [oc.decode(mask) for _ in range(20)]
+    out["oracle_encode_us"] = round(1e6 * float(np.median(ce)), 1)
+    out["oracle_decode_us"] = round(1e6 * float(np.median(cd)), 1)
+    out["note"] = (f"k={k} m={m} {ec_type}, one {size} B file; CLI = fresh interpreter per "
+                   f"call, median of {reps}, decode from {k} of {k + m} fragment files "
+                   "(m random dropped); in-process = ECDriver calls, median of 20; oracle = "
+                   "scalar C restatement, 1 core, median of 20")
+    return {"config0": out}
+
+
+# ---------------- decode with erasures that change every step ----------------
+
+def fresh_decode(args, codec, stripes, objs, out, stream, B, rank):
+    """`--fresh-steps` decode steps whose masks are drawn anew each step (seed
+    + rank + step, outside the clock) and handed to the call inside it, so
+    the per-call work the reference does in every decode (pyeclib_c.c:878:
+    first-k choice, inverse, tables, descriptors, their H2D) is timed.  The
+    GPU is idle when each step starts, so the event span covers the host
+    work before the launch too.  Every step's output is compared with the
+    objects (on the GPU, untimed); returns the timing dict and all-ok."""
+    import torch
+    k, m, n = args.k, args.m, args.obj_bytes
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.fresh_steps)]
+    gpu_ms, wall_ms, ok = [], [], True
+    for i in range(args.fresh_steps):
+        rng = np.random.Generator(np.random.PCG64(SEED + rank + 1000 * (i + 1)))
+        masks = erasure_masks(rng, B, k, m, args.erasures)
+        out.zero_()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev[i][0].record(stream)
+        codec.decode(stripes, n, masks, out)
+        ev[i][1].record(stream)
+        torch.cuda.synchronize()
+        wall_ms.append(1e3 * (time.perf_counter() - t0))
+        gpu_ms.append(ev[i][0].elapsed_time(ev[i][1]))
+        ok = ok and bool(torch.equal(out[:, :n], objs[:, :n]))
+    return {"decode_fresh_ms": round(float(np.mean(gpu_ms)), 4),
+            "decode_fresh_first_ms": round(gpu_ms[0], 4),
+            "decode_fresh_wall_ms": round(float(np.mean(wall_ms)), 4),
+            "decode_fresh_steps": args.fresh_steps,
+            "decode_fresh_note": "new erasure masks every step (PCG64 seed + rank + 1000*step); "
+                                 "event span from an idle GPU, host descriptor build + H2D + "
+                                 "kernel; every step's objects compared with the originals"}, ok
 
 
 def main():
@@ -460,12 +599,18 @@ def main():
         sys.exit(relaunch_ranks(args))
     if args.dry_run:
         return dry_run(args)
-    import torch
-    from pyeclib_amd import _native, batch, shard
+    from pyeclib_amd import placement, shard
     world, rank, local = shard.rank_info()
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    shard.init("nccl")
+    dev_idx = shard.device_index(local, args.same_device)
+    # CPUs first, before anything starts the HIP runtime (its threads inherit
+    # the mask), then the pinned buffers are first touched on that node
+    numa = {"bound": False, "reason": "--no-numa"} if args.no_numa else \
+        placement.bind_to_gpu_numa(dev_idx)
+    import torch
+    from pyeclib_amd import _native, batch
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
+    shard.init("gloo")  # bookkeeping only: no RCCL communicator
     if world != args.gpus and rank == 0:
         print(f"bench.py: --gpus {args.gpus} but the launcher started {world} ranks; "
               f"reporting n_gpus={world}", file=sys.stderr)
@@ -532,7 +677,7 @@ def main():
     events[-1].record(stream)
     torch.cuda.synchronize()
     shard.barrier()
-    elapsed = shard.max_over_ranks(time.perf_counter() - t0, device=dev)
+    elapsed = shard.max_over_ranks(time.perf_counter() - t0)
 
     enc_ms = float(np.mean([events[2 * i].elapsed_time(events[2 * i + 1])
                             for i in range(args.steps)]))
@@ -547,12 +692,14 @@ def main():
     #   encode: read the object (L), write m payloads + m headers
     #   decode: read k payloads, write the object
     #   reconstruct: read k payloads, write one fragment
-    enc_bytes = B * (n + m * (bs + 80))
-    two_bytes = B * (k * bs + n) if two == "decode" else B * (k * bs + bs + 80)
+    enc_read = B * n
+    two_read = B * k * bs
+    enc_bytes = enc_read + B * m * (bs + 80)
+    two_bytes = two_read + (B * n if two == "decode" else B * (bs + 80))
     kernels = {
-        "encode": {"ms": round(enc_ms, 4), "bytes": enc_bytes,
+        "encode": {"ms": round(enc_ms, 4), "bytes": enc_bytes, "read_bytes": enc_read,
                    "GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 1)},
-        two: {"ms": round(dec_ms, 4), "bytes": two_bytes,
+        two: {"ms": round(dec_ms, 4), "bytes": two_bytes, "read_bytes": two_read,
               "GBps": round(two_bytes / (dec_ms * 1e-3) / 1e9, 1)},
     }
     dom = two if dec_ms >= enc_ms else "encode"
@@ -565,11 +712,18 @@ def main():
     pmc_ok = pmc.get("library_id") == lib_id
     traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch") if pmc_ok else None
     achieved = kernels[dom]["GBps"]
+
+    def read_frac(kk):
+        v = kernels[kk]
+        return round(v["read_bytes"] / (v["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+
     roofline = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "algorithmic_bytes": kernels[dom]["bytes"],
+                "read_frac": read_frac(dom),
                 "frac_by_kernel": {kk: round(v["GBps"] / HBM_PEAK_GBPS, 4)
                                    for kk, v in kernels.items()},
+                "read_frac_by_kernel": {kk: read_frac(kk) for kk in kernels},
                 "traffic_by_kernel": ({kk: pmc.get(kk, {}).get("hbm_bytes_per_launch")
                                        for kk in kernels} if pmc_ok else None),
                 "library_id": lib_id}
@@ -596,12 +750,24 @@ def main():
                                   else "reconstruct (1 fragment)")
                                + f", {n} B objects, batch {B} per GPU, device-resident",
                    "k": k, "m": m, "object_bytes": n, "batch_per_gpu": B,
-                   "erasures": args.erasures, "parallelism": f"objects sharded over {world} GPU"},
+                   "erasures": args.erasures, "parallelism": f"objects sharded over {world} GPU"
+                   + (" (all ranks on cuda:0)" if args.same_device and world > 1 else "")},
         "encode_GiBps": round(n_total * n / (enc_ms * 1e-3) / 2**30, 3),
         f"{two}_GiBps": round(n_total * n / (dec_ms * 1e-3) / 2**30, 3),
         "kernels": kernels,
         "roofline": roofline,
     }
+    if args.same_device and world > 1:
+        result["same_device"] = True
+
+    # ---- erasures that change every step (untimed by the headline) ----
+    fresh_ok = True
+    if two == "decode" and args.fresh_steps > 0:
+        fresh, fresh_ok = fresh_decode(args, codec, stripes, objs, out, stream, B, rank)
+        result.update(fresh)
+        # the headline batch is decoded again so the oracle check below sees it
+        codec.decode(stripes, n, masks, out)
+        torch.cuda.synchronize()
 
     # ---- verification of the timed batch (every object), and the CPU baseline ----
     bad = []
@@ -613,11 +779,9 @@ def main():
         t_enc, t_two, bad, src = oracle_pass(args, host, two_masks, dests, gpu_frags,
                                              gpu_second, sample=B)
         del gpu_frags, gpu_second
-    ok = torch.tensor([0 if bad else 1], dtype=torch.int32, device=dev)
-    if world > 1:
-        import torch.distributed as dist
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    verified = bool(ok.item()) and not args.no_verify
+    if not fresh_ok:
+        bad.append((-1, "fresh-erasure decode"))
+    verified = bool(shard.min_over_ranks(0 if bad else 1)) and not args.no_verify
     result["verified"] = verified
     if not args.no_verify:
         result["verified_objects"] = n_total
@@ -625,15 +789,22 @@ def main():
         print(f"rank {rank}: {len(bad)} mismatches vs the oracle, first: {bad[:5]}",
               file=sys.stderr, flush=True)
 
+    numa_all = numa
+    if rank == 0:
+        result["placement"] = {"rank0": numa, "cpu_affinity": len(os.sched_getaffinity(0))}
+
     if rank == 0 and not args.no_host and w == 16:
         result.update(host_resident(args, codec, host, stripes, masks, fs, bs))
         result.update(single_object_calls(args))
+    if rank == 0 and args.config0:
+        result.update(config0_cli(args))
 
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline and (world == 1 or args.cpu_baseline_all):
         sample = min(args.cpu_sample or B, B)
         if t_enc is None or sample != B:
             t_enc, t_two, _, src = oracle_pass(args, host, two_masks, dests, sample=sample)
-        workers = max(1, min(CPU_WORKERS_MAX, len(os.sched_getaffinity(0)), sample))
+        affinity = len(os.sched_getaffinity(0))
+        workers = max(1, min(affinity, CPU_WORKERS_PER_GPU * world, sample))
         t_par = cpu_parallel(args, host, two_masks, dests, sample, workers)
         one = 2 * sample * n / (t_enc + t_two) / 2**30
         result["cpu_baseline"] = {
@@ -642,6 +813,8 @@ def main():
             "sample": f"{sample} objects x {n} B: encode + {two} ({src}, {args.ec_type}), "
                       f"{workers} single-threaded worker processes (objects split evenly)",
             "cpu_model": cpu_model(),
+            "affinity_cpus": affinity,
+            "numa_node": numa_all.get("numa_node"),
             "single_core_value": round(one, 4),
             "single_core_encode_GiBps": round(sample * n / t_enc / 2**30, 4),
             f"single_core_{two}_GiBps": round(sample * n / t_two / 2**30, 4),
@@ -650,9 +823,7 @@ def main():
         }
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    shard.finish()
     if not args.no_verify and not verified:
         sys.exit(3)
 

@@ -228,6 +228,16 @@ int ecamd_reconstruct_host_batch(int desc, const void *h_frags, uint64_t frag_st
 /* Device ordinal used by this process (hipGetDevice at create time). */
 int ecamd_device(int desc);
 
+/* Does a batch layout fit the kernels' 32-bit buffer offsets?  0, or
+ * -EINVALIDPARAMS when it does not: k*blocksize + 16 (an object's slices;
+ * decode's output window holds 2^31 - 1 bytes), (k+m)*frag_stride (a stripe's
+ * fragments) or the batch's 4 KiB work items pass their limit.  Every
+ * encode / decode / reconstruct entry point (single object or batch) applies
+ * it and returns -EINVALIDPARAMS instead of launching; needs no GPU.  w = 16
+ * (rs_vand) or 8 (ISA-L codes). */
+int ecamd_layout_supported(int k, int m, int w, uint64_t obj_len, uint64_t frag_stride,
+                           uint64_t n_obj);
+
 #ifdef __cplusplus
 }
 #endif

@@ -140,6 +140,9 @@ _sig = {
     "liberasurecode_get_version": (ctypes.c_uint32, []),
     "ecamd_blocksize": (ctypes.c_uint64, [ctypes.c_int, ctypes.c_uint64]),
     "ecamd_device": (ctypes.c_int, [ctypes.c_int]),
+    "ecamd_layout_supported": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_uint64, ctypes.c_uint64,
+                                              ctypes.c_uint64]),
     "ecamd_encode_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
                                           ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p,
                                           ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,

@@ -89,6 +89,23 @@ class BatchCodec:
             _native.raise_error(ret, fn)
 
     @staticmethod
+    def _check_rows(fn: str, x: Any, rows: int | None = None) -> None:
+        """A (n_obj, rows, stride) or (n_obj, stride) uint8 tensor must be
+        packed the way the C side walks it: bytes contiguous, and -- for
+        per-object groups of `rows` fragments -- each object's group at
+        rows * stride(1) (the C API takes only the fragment stride, so a
+        strided view such as stripes[:, :k] would be read as the wrong bytes)."""
+        if x is None or not hasattr(x, "stride"):
+            return
+        dims = x.dim() if hasattr(x, "dim") else len(x.shape)
+        if int(x.stride(dims - 1)) != 1:
+            _native.raise_error(-_native.EINVALIDPARAMS, fn)
+        if rows is not None:
+            if dims != 3 or int(x.shape[1]) != rows or \
+                    (int(x.shape[0]) > 1 and int(x.stride(0)) != rows * int(x.stride(1))):
+                _native.raise_error(-_native.EINVALIDPARAMS, fn)
+
+    @staticmethod
     def _check_count(fn: str, n_obj: int, *arrays: Any) -> None:
         """n_obj per-object entries must fit every tensor they index (the C
         entry points trust the caller's sizes)."""
@@ -104,6 +121,8 @@ class BatchCodec:
         fragments."""
         n_obj = int(objs.shape[0])
         self._check_count("ecamd_encode_batch", n_obj, parity, data)
+        for x in (objs, parity, data):
+            self._check_rows("ecamd_encode_batch", x)
         fs = frag_stride if frag_stride is not None else int(parity.stride(1))
         ret = _native.lib.ecamd_encode_batch(
             self.handle.desc, _ptr(objs), _stride0(objs, obj_len), obj_len, n_obj,
@@ -116,6 +135,8 @@ class BatchCodec:
         """frags: (n_obj, k+m, frag_stride) stripes; out: (n_obj, obj_stride)."""
         n_obj = len(avail_masks)
         self._check_count("ecamd_decode_batch", n_obj, frags, out)
+        for x in (frags, out):
+            self._check_rows("ecamd_decode_batch", x)
         masks = (ctypes.c_uint32 * n_obj)(*avail_masks)
         fs = int(frags.stride(1))
         ret = _native.lib.ecamd_decode_batch(
@@ -130,6 +151,8 @@ class BatchCodec:
         if len(dest) != n_obj:
             _native.raise_error(-_native.EINVALIDPARAMS, "ecamd_reconstruct_batch")
         self._check_count("ecamd_reconstruct_batch", n_obj, frags, out)
+        for x in (frags, out):
+            self._check_rows("ecamd_reconstruct_batch", x)
         masks = (ctypes.c_uint32 * n_obj)(*avail_masks)
         dst = (ctypes.c_int * n_obj)(*dest)
         fs = int(frags.stride(1))
@@ -143,6 +166,8 @@ class BatchCodec:
         (n_obj, m, frag_stride) in (pinned) host memory."""
         n_obj = int(objs.shape[0])
         self._check_count("ecamd_encode_host_batch", n_obj, parity)
+        self._check_rows("ecamd_encode_host_batch", objs)
+        self._check_rows("ecamd_encode_host_batch", parity, self.m)
         ret = _native.lib.ecamd_encode_host_batch(
             self.handle.desc, _ptr(objs), _stride0(objs, obj_len), obj_len, n_obj,
             _ptr(parity), int(parity.stride(1)))
@@ -157,6 +182,8 @@ class BatchCodec:
         self._check_count("ecamd_decode_host_batch", n_obj, frags, out)
         if hasattr(frags, "shape") and int(frags.shape[1]) != self.k:
             _native.raise_error(-_native.EINVALIDPARAMS, "ecamd_decode_host_batch")
+        self._check_rows("ecamd_decode_host_batch", frags, self.k)
+        self._check_rows("ecamd_decode_host_batch", out)
         masks = (ctypes.c_uint32 * n_obj)(*avail_masks)
         ret = _native.lib.ecamd_decode_host_batch(
             self.handle.desc, _ptr(frags), int(frags.stride(1)), obj_len, n_obj, masks,
@@ -171,6 +198,8 @@ class BatchCodec:
         if len(dest) != n_obj or (hasattr(frags, "shape") and int(frags.shape[1]) != self.k):
             _native.raise_error(-_native.EINVALIDPARAMS, "ecamd_reconstruct_host_batch")
         self._check_count("ecamd_reconstruct_host_batch", n_obj, frags, out)
+        self._check_rows("ecamd_reconstruct_host_batch", frags, self.k)
+        self._check_rows("ecamd_reconstruct_host_batch", out)
         masks = (ctypes.c_uint32 * n_obj)(*avail_masks)
         dst = (ctypes.c_int * n_obj)(*dest)
         ret = _native.lib.ecamd_reconstruct_host_batch(

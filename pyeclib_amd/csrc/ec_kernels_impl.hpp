@@ -554,8 +554,9 @@ __device__ __forceinline__ void enc_item_pos(const EncodeParams& p, uint32_t w, 
 constexpr int kEdgeGroup = 1;
 
 // Edge item: payload tail and chunks reaching the zero padding past obj_len
-// (liberasurecode's prepare_fragments_for_encode zero-fills).
-template <class F, int K, int NR>
+// (liberasurecode's prepare_fragments_for_encode zero-fills).  DATA: the
+// padded input chunks are also the data fragments' payload bytes.
+template <class F, int K, int NR, bool DATA>
 __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t e) {
   const uint32_t o = e / p.edge_tiles;
   const uint32_t t = (p.tiles + (e - o * p.edge_tiles)) * kTile + threadIdx.x * 16;
@@ -577,6 +578,14 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
 #pragma unroll
     for (int j = 0; j < G; ++j)
       if (j0 + j < K) F::template mac<true>(F::kb(0), (j0 + j) * F::kTableBytes, x[j], s);
+    if constexpr (DATA) {
+#pragma unroll
+      for (int j = 0; j < G; ++j)
+        if (j0 + j < K)
+          store_partial(p.data + static_cast<uint64_t>(o) * p.stripe_stride +
+                            static_cast<uint64_t>(j0 + j) * p.frag_stride + kHeaderBytes + t,
+                        x[j], rem);
+    }
     __builtin_amdgcn_sched_barrier(0);
   }
   F::pin(s);
@@ -588,9 +597,14 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
 
 // Interior encode: object slices streamed in (default cache policy --
 // neighbouring slices share 128-B lines, which L2 then serves twice), parity
-// chunks stored nontemporal and line-aligned.  NOCOMP: memory-only probe
-// (inputs XORed, no lookups; wrong parity) for the benchmark shape.
-template <class F, int K, int NR, bool NOCOMP = false>
+// chunks stored nontemporal and line-aligned.  DATA (full-stripe encode,
+// liberasurecode_encode's k data + m parity fragments, pyeclib_c.c:544-560):
+// each input chunk, already in registers for its products, is also stored to
+// its data fragment's line-aligned payload before the registers are refilled
+// -- one pass over the object instead of a separate copy.  NOCOMP:
+// memory-only probe (inputs XORed, no lookups; wrong parity) for the
+// benchmark shape.
+template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false>
 __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
   constexpr int NB = stream_bufs<K>();
   const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
@@ -611,6 +625,8 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
     uint32_t on, xn;
     enc_item_pos(p, wn, on, xn);
     const Rsrc nxt = rsrc(p.objs + static_cast<uint64_t>(on) * p.obj_stride, wn == w ? 0 : -1);
+    Rsrc dat;
+    if constexpr (DATA) dat = rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride);
     typename F::Acc s;
     F::zero(s);
 #pragma unroll
@@ -625,6 +641,7 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
         } else {
           F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[j % NB], s);
         }
+        if constexpr (DATA) buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x, buf[j % NB]);
       }
       if (j + NB < KP) {
         if (j + NB < K) buf[j % NB] = buf_ld<true>(cur, lane16, (j + NB) * p.bs + x);
@@ -647,7 +664,7 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
 
 // Headers and edge items of an encode, block b taking objects / items
 // b, b + G, ... (b counted from `first`, G = `step` blocks).  Tables are at LDS 0.
-template <class F, int K, int NR>
+template <class F, int K, int NR, bool DATA>
 __device__ __forceinline__ void encode_edges(const EncodeParams& p, uint32_t first, uint32_t step) {
   if (p.headers != nullptr && p.row0 == 0)
     for (uint32_t o = first; o < p.n_obj; o += step) {
@@ -655,7 +672,8 @@ __device__ __forceinline__ void encode_edges(const EncodeParams& p, uint32_t fir
       block_headers(p.parity + base, p.frag_stride, p.headers + K * kHeaderBytes, p.m);
       if (p.data != nullptr) block_headers(p.data + base, p.frag_stride, p.headers, K);
     }
-  for (uint32_t e = first; e < p.n_obj * p.edge_tiles; e += step) encode_edge_item<F, K, NR>(p, e);
+  for (uint32_t e = first; e < p.n_obj * p.edge_tiles; e += step)
+    encode_edge_item<F, K, NR, DATA>(p, e);
 }
 
 // One launch per encode: the headers and edge items, in the blocks counted
@@ -665,13 +683,13 @@ __device__ __forceinline__ void encode_edges(const EncodeParams& p, uint32_t fir
 // profiles/r02l_timeline.txt): with the edges in a launch of their own on a
 // side stream, the fork / join left the GPU idle 25-32 us between
 // consecutive interior kernels.
-template <class F, int K, int NR, bool NOCOMP = false>
+template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false>
 __global__ void __launch_bounds__(kThreadsPerBlock)
     __attribute__((amdgpu_waves_per_eu(kEncodeOcc, 8))) encode_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
   __syncthreads();
-  if (p.fused_edges) encode_edges<F, K, NR>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
-  encode_interior<F, K, NR, NOCOMP>(p);
+  if (p.fused_edges) encode_edges<F, K, NR, DATA>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
+  encode_interior<F, K, NR, NOCOMP, DATA>(p);
 }
 
 // Headers and edge items of an encode in a launch of their own (the
@@ -680,7 +698,7 @@ template <class F, int K, int NR>
 __global__ void __launch_bounds__(kThreadsPerBlock) encode_edge_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
   __syncthreads();
-  encode_edges<F, K, NR>(p, blockIdx.x, gridDim.x);
+  encode_edges<F, K, NR, false>(p, blockIdx.x, gridDim.x);
 }
 
 // ---------------- encode with the parity CRC fused (inline_crc32) ----------------
@@ -753,7 +771,7 @@ __device__ __forceinline__ uint32_t* crc_part_at(const EncodeParams& p, uint32_t
 
 // Interior with the parity CRC: block b streams the contiguous items
 // [n*b/G, n*(b+1)/G) (ec_crc.hip run_begin), otherwise as encode_interior.
-template <class F, int K, int NR>
+template <class F, int K, int NR, bool DATA>
 __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
   constexpr int NB = stream_bufs<K>();
   constexpr uint32_t base = crc_lds_base<F, K>();
@@ -780,11 +798,16 @@ __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
     uint32_t on, xn;
     enc_item_pos(p, wn, on, xn);
     const Rsrc nxt = rsrc(p.objs + static_cast<uint64_t>(on) * p.obj_stride, wn == w ? 0 : -1);
+    Rsrc dat;
+    if constexpr (DATA) dat = rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride);
     typename F::Acc s;
     F::zero(s);
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
-      if (j < K) F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[j % NB], s);
+      if (j < K) {
+        F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[j % NB], s);
+        if constexpr (DATA) buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x, buf[j % NB]);
+      }
       if (j + NB < KP) {
         if (j + NB < K) buf[j % NB] = buf_ld<true>(cur, lane16, (j + NB) * p.bs + x);
       } else if (j + NB - KP < K) {
@@ -813,7 +836,7 @@ __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
   }
 }
 
-template <class F, int K, int NR>
+template <class F, int K, int NR, bool DATA = false>
 __global__ void __launch_bounds__(kThreadsPerBlock)
     __attribute__((amdgpu_waves_per_eu(kEncodeCrcOcc, 8))) encode_crc_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
@@ -821,13 +844,14 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
   __syncthreads();
   // headers and edge items as encode_kernel; the edge tiles' CRC is taken by
   // crc_finish_kernel from the parity just written
-  encode_edges<F, K, NR>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
-  encode_crc_interior<F, K, NR>(p);
+  encode_edges<F, K, NR, DATA>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
+  encode_crc_interior<F, K, NR, DATA>(p);
 }
 
 // Data fragments (optional output of encode): the k padded object slices
 // copied into their fragment payloads.  Item = (object, fragment, 4 KiB).
-__global__ void __launch_bounds__(kThreadsPerBlock) copy_data_kernel(EncodeParams p) {
+__global__ void __launch_bounds__(kThreadsPerBlock) __attribute__((unused))
+    copy_data_kernel(EncodeParams p) {
   const uint32_t per_frag = (p.bs + kTile - 1) / kTile;
   const uint32_t per_obj = p.k * per_frag;
   const uint32_t items = p.n_obj * per_obj;
@@ -1294,6 +1318,8 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   p.tiles = static_cast<uint32_t>(last_room(p.bs, p.obj_len, K) / kTile);
   p.edge_tiles = (p.bs + kTile - 1) / kTile - p.tiles;
   constexpr size_t lds = K * F::kTableBytes;
+  // data fragments are written by the first pass (rows 0..3) only
+  const bool data = p.data != nullptr && p.row0 == 0;
   bool probe = false;
   int per_cu = kEncodePerCu;
   if constexpr (K == 10 && NR == 4) {
@@ -1308,8 +1334,11 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     const uint32_t items = std::max({p.n_obj * p.tiles, p.n_obj * p.edge_tiles,
                                      p.headers ? p.n_obj : 0u});
     int grid = 0;
-    e = launch(encode_crc_kernel<F, K, NR>, p, crc_lds_bytes<F, K>(), items, stream,
-               env_int("ECAMD_CRC_PER_CU", kEncodePerCu), false, &grid);  // A/B knob
+    const int crc_per_cu = env_int("ECAMD_CRC_PER_CU", kEncodePerCu);  // A/B knob
+    e = data ? launch(encode_crc_kernel<F, K, NR, true>, p, crc_lds_bytes<F, K>(), items, stream,
+                      crc_per_cu, false, &grid)
+             : launch(encode_crc_kernel<F, K, NR>, p, crc_lds_bytes<F, K>(), items, stream,
+                      crc_per_cu, false, &grid);
     if (e != hipSuccess) return e;
     CrcFinishParams fp{};
     fp.parity = p.parity;
@@ -1326,19 +1355,21 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     fp.tiles = p.tiles;
     fp.edge_tiles = p.edge_tiles;
     fp.grid = static_cast<uint32_t>(grid);
-    if ((e = launch_crc_finish(fp, stream)) != hipSuccess) return e;
-    if (p.data == nullptr || p.row0 != 0) return hipSuccess;
-    return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + kTile - 1) / kTile), stream);
+    return launch_crc_finish(fp, stream);
   }
   if (!env_flag("ECAMD_EDGE_SIDE", false)) {
-    // one launch: interior stream + edge items + headers
+    // one launch: interior stream + edge items + headers (+ the data
+    // fragments when asked: stored from the input registers)
     p.fused_edges = 1;
     const uint32_t items = std::max({p.n_obj * p.tiles, p.n_obj * p.edge_tiles,
                                      p.headers ? p.n_obj : 0u});
     if constexpr (K == 10 && NR == 4)
       if (probe) return launch(encode_kernel<F, K, NR, true>, p, lds, items, stream, per_cu);
+    if (data && !env_flag("ECAMD_DATA_COPY", false))
+      return launch(encode_kernel<F, K, NR, false, true>, p, lds, items, stream, per_cu);
     e = launch(encode_kernel<F, K, NR>, p, lds, items, stream, per_cu);
-    if (e != hipSuccess || p.data == nullptr || p.row0 != 0) return e;
+    if (e != hipSuccess || !data) return e;
+    // ECAMD_DATA_COPY=1 (A/B): the data fragments in a copy launch of their own
     return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + kTile - 1) / kTile), stream);
   }
   p.fused_edges = 0;
@@ -1354,7 +1385,7 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
         return launch(encode_edge_kernel<F, K, NR>, p, lds,
                       std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u), s);
       });
-  if (e != hipSuccess || p.data == nullptr || p.row0 != 0) return e;
+  if (e != hipSuccess || !data) return e;
   return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + kTile - 1) / kTile), stream);
 }
 

@@ -66,6 +66,7 @@ const Code* code_of(int backend_id) {
 }
 constexpr int kRing = 4;
 constexpr int kHostStreams = 4;  // host-resident pipeline streams (H2D / kernel / D2H in flight)
+constexpr int kCrcPartSlots = 8;  // fused parity CRC partials: one buffer per stream
 
 inline uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
 
@@ -272,6 +273,15 @@ struct Instance {
   uint32_t pool_slots = 0, pool_used = 0;
   uint64_t pool_gen = 1;  // bumped whenever slots are recycled
   std::unordered_map<uint64_t, uint32_t> pool_index;
+  // table sets of patterns new in this call: built on the host into
+  // pool_stage (slots pool_stage_first..), uploaded by pool_commit with ONE
+  // async copy on the call's stream ahead of its launch; pool_ev marks the
+  // last such copy for launches on other streams
+  std::vector<uint8_t> pool_stage;
+  uint32_t pool_stage_first = 0;
+  hipEvent_t pool_ev = nullptr;
+  hipStream_t pool_ev_stream = nullptr;
+  bool pool_ev_pending = false;
   DevBuf scratch;  // single-object staging
   PinBuf pin;      // single-object staging, zero-copy (small objects)
   RingSlot ring[kRing];
@@ -282,9 +292,16 @@ struct Instance {
   hipEvent_t hdone[kHostStreams] = {};
   std::map<uint64_t, DevBuf> crc_tables;  // payload size -> CrcTables (device)
   std::map<uint64_t, DevBuf> crc_finish;  // payload size -> CrcFinishTables (device)
-  DevBuf crc_part;                        // fused parity CRC: run partials
-  hipStream_t crc_part_stream = nullptr;  // stream of the last launch using crc_part
-  bool crc_part_used = false;
+  // fused parity CRC run partials, one buffer per launch stream: a launch
+  // reads and writes its own stream's buffer, so launches on different
+  // streams (the staged host pipeline deals chunks over 3) never share one
+  // and need no device-wide wait between them
+  struct CrcPart {
+    hipStream_t stream = nullptr;
+    bool used = false;
+    DevBuf buf;
+  } crc_part[kCrcPartSlots];
+  int crc_part_victim = 0;
 
   // bytes of one table set (k inputs x up to 4 rows)
   size_t table_bytes() const { return static_cast<size_t>(k) * table_bytes_per_input(code.w); }
@@ -299,6 +316,10 @@ struct Instance {
       }
     for (auto& e : hdone)
       if (e) (void)hipEventDestroy(e);
+    if (pool_ev) {
+      (void)hipEventSynchronize(pool_ev);
+      (void)hipEventDestroy(pool_ev);
+    }
     dec_cache.release();
     rec_cache.release();
     hdr_cache.release();
@@ -317,7 +338,7 @@ struct Instance {
     for (auto& b : hbuf) b.release();
     for (auto& kv : crc_tables) kv.second.release();
     for (auto& kv : crc_finish) kv.second.release();
-    crc_part.release();
+    for (auto& c : crc_part) c.buf.release();
     if (stream) (void)hipStreamDestroy(stream);
   }
 
@@ -447,6 +468,40 @@ hipError_t upload_done(Instance& I, Upload& u, hipStream_t s) {
   return hipSuccess;
 }
 
+// The fused parity CRC's partials buffer for launches on stream s, at least
+// `bytes` long.  A stream keeps its slot; a new stream takes a free slot, or
+// -- all taken -- the round-robin victim once the device is idle (its stream
+// may be gone).  Growing a slot waits for its own stream only.
+hipError_t crc_part_for(Instance& I, hipStream_t s, size_t bytes, uint32_t** out) {
+  Instance::CrcPart* slot = nullptr;
+  for (auto& c : I.crc_part)
+    if (c.used && c.stream == s) {
+      slot = &c;
+      break;
+    }
+  hipError_t e;
+  if (!slot) {
+    for (auto& c : I.crc_part)
+      if (!c.used) {
+        slot = &c;
+        break;
+      }
+    if (!slot) {
+      slot = &I.crc_part[I.crc_part_victim];
+      I.crc_part_victim = (I.crc_part_victim + 1) % kCrcPartSlots;
+      if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+    }
+    slot->stream = s;
+    slot->used = true;
+  }
+  if (bytes > slot->buf.cap) {
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    if ((e = slot->buf.ensure(bytes)) != hipSuccess) return e;
+  }
+  *out = static_cast<uint32_t*>(slot->buf.p);
+  return hipSuccess;
+}
+
 template <class T>
 void key_append(std::vector<uint8_t>& key, const T* p, size_t n) {
   const uint8_t* b = reinterpret_cast<const uint8_t*>(p);
@@ -558,10 +613,13 @@ void missing_rows(const Instance& I, const int* avail, int dest, std::vector<int
 }
 
 // Wait for every launch that may read the pool, then forget all patterns.
+// (Staged sets were committed by the flush that precedes every recycle.)
 void pool_recycle(Instance& I) {
   (void)hipDeviceSynchronize();
   I.pool_index.clear();
   I.pool_used = 0;
+  I.pool_stage.clear();
+  I.pool_ev_pending = false;
   ++I.pool_gen;
 }
 
@@ -593,20 +651,56 @@ int pool_slot(Instance& I, uint32_t avail_mask, const int* avail, int dest, uint
   if (I.pool_used == I.pool_slots) return kPoolFull;
   if (!pattern_rows(I, avail, dest, rows, out_idx)) return -EINSUFFFRAGS;
   const uint32_t s = I.pool_used++;
-  std::vector<uint8_t> host(set_bytes * I.passes, 0);
+  // staged for pool_commit: the new slots of a call are consecutive
+  if (I.pool_stage.empty()) I.pool_stage_first = s;
+  const size_t at = I.pool_stage.size();
+  I.pool_stage.resize(at + set_bytes * I.passes, 0);
+  uint8_t* host = I.pool_stage.data() + at;
   const int nrows = static_cast<int>(out_idx.size());
   for (uint32_t p = 0; p * kRowsPerPass < static_cast<uint32_t>(nrows); ++p) {
     const int r0 = p * kRowsPerPass;
     const int nr = std::min(kRowsPerPass, nrows - r0);
     build_tables(I.code.w, &rows[static_cast<size_t>(r0) * I.k], nr, I.k, &host[p * set_bytes]);
   }
-  // The slot is unused by any in-flight kernel, so a synchronous upload is safe.
-  hipError_t e = hipMemcpy(I.pool.b() + static_cast<size_t>(s) * set_bytes * I.passes,
-                           host.data(), host.size(), hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_errno(e);
   I.pool_index.emplace(key, s);
   *slot = s;
   return 0;
+}
+
+// Upload the table sets staged by pool_slot (one async copy through the ring
+// on the launch stream: no kernel reads a new slot before the copy, and no
+// in-flight kernel reads it at all -- slots are only rewritten after
+// pool_recycle's device-wide wait).  Then make `stream` wait for any table
+// copy still running on another stream.  Call before every launch that
+// reads the pool.
+hipError_t pool_commit(Instance& I, hipStream_t stream) {
+  hipError_t e = hipSuccess;
+  if (!I.pool_stage.empty()) {
+    const size_t n = I.pool_stage.size();
+    RingSlot* r = I.ring_acquire(n, &e);
+    if (!r) return e;
+    std::memcpy(r->host, I.pool_stage.data(), n);
+    const size_t slot_bytes = I.table_bytes() * I.passes;
+    e = hipMemcpyAsync(I.pool.b() + static_cast<size_t>(I.pool_stage_first) * slot_bytes, r->host,
+                       n, hipMemcpyHostToDevice, stream);
+    I.pool_stage.clear();
+    const hipError_t er = I.ring_release(r, stream);
+    if (e != hipSuccess) return e;
+    if (er != hipSuccess) return er;
+    if (!I.pool_ev && (e = hipEventCreateWithFlags(&I.pool_ev, hipEventDisableTiming)) != hipSuccess)
+      return e;
+    if ((e = hipEventRecord(I.pool_ev, stream)) != hipSuccess) return e;
+    I.pool_ev_stream = stream;
+    I.pool_ev_pending = true;
+    return hipSuccess;
+  }
+  if (I.pool_ev_pending && I.pool_ev_stream != stream) {
+    if (hipEventQuery(I.pool_ev) == hipSuccess)
+      I.pool_ev_pending = false;
+    else
+      e = hipStreamWaitEvent(stream, I.pool_ev, 0);
+  }
+  return e;
 }
 
 // First k available indices of a mask; returns count found.
@@ -678,6 +772,7 @@ uint32_t passes_of(const DecodeJob& J, const DescBatch& B, int o0, int o1) {
 hipError_t launch_range(Instance& I, const DecodeJob& J, int o0, int o1, uint32_t passes,
                         const uint8_t* dev, uint64_t bs, hipStream_t stream) {
   const int n = o1 - o0;
+  if (hipError_t e = pool_commit(I, stream); e != hipSuccess) return e;
   for (uint32_t p = 0; p < passes; ++p) {
     DecodeParams P{};
     P.frags = J.frags + static_cast<uint64_t>(o0) * J.stripe_stride;
@@ -722,6 +817,19 @@ int flush_range(Instance& I, const DecodeJob& J, const DescBatch& B, int o0, int
   return e2 == hipSuccess ? 0 : hip_errno(e2);
 }
 
+// The kernels address an object's bytes and a stripe's fragments through
+// buffer descriptors with 32-bit offsets (ec_kernels_impl.hpp): j*bs + x for
+// object slices (decode's output descriptor holds 2^31 - 1 records, so that
+// voffset 2^31 drops a store), i*frag_stride + 80 + x inside a stripe
+// (2^32 - 1 records), and 32-bit item indices.  A layout past those limits
+// would wrap with no error, so it is refused before anything is launched.
+bool layout_fits(int k, int m, uint64_t bs, uint64_t frag_stride, uint64_t n_obj) {
+  if (bs > 0xFFFFFFF0ull) return false;
+  if (static_cast<uint64_t>(k) * bs + 16 > 0x7FFFFFFFull) return false;
+  if (static_cast<uint64_t>(k + m) * frag_stride > 0xFFFFFFF0ull) return false;
+  return n_obj * (bs / 4096 + 1) < (1ull << 31);
+}
+
 // Shared decode / reconstruct launcher (caller holds I.mu, device set).
 //
 // Every object needs the table set of its erasure pattern in the device pool.
@@ -738,6 +846,8 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
   if (J.frag_stride % 16 || J.frag_stride < kHeaderBytes + round16(bs)) return -EINVALIDPARAMS;
   if (J.stripe_stride % 16 || reinterpret_cast<uintptr_t>(J.frags) % 16) return -EINVALIDPARAMS;
   if (J.dest && (J.out_stride % 16 || reinterpret_cast<uintptr_t>(J.out) % 16))
+    return -EINVALIDPARAMS;
+  if (!layout_fits(k, I.m, bs, J.frag_stride, static_cast<uint64_t>(J.n_obj)))
     return -EINVALIDPARAMS;
   for (int o = 0; o < J.n_obj; ++o) {
     if (__builtin_popcount(J.masks[o] & ((n >= 32 ? 0u : (1u << n)) - 1u)) < k)
@@ -877,7 +987,7 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
   if (n_obj > 1 && (obj_stride < obj_len || obj_stride % 16)) return -EINVALIDPARAMS;
   if (reinterpret_cast<uintptr_t>(parity) % 16 || reinterpret_cast<uintptr_t>(data) % 16)
     return -EINVALIDPARAMS;
-  if (bs > 0xFFFFFFF0ull) return -EINVALIDPARAMS;
+  if (!layout_fits(k, m, bs, frag_stride, static_cast<uint64_t>(n_obj))) return -EINVALIDPARAMS;
   const size_t hdr_bytes = headers ? static_cast<size_t>(k + m) * kHeaderBytes : 0;
   Upload u;
   hipError_t e;
@@ -904,6 +1014,7 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
   const bool fused_crc = crc && !(fused_env && fused_env[0] == '0');
   const void* crc_maps = nullptr;
   const void* crc_fin = nullptr;
+  uint32_t* crc_part = nullptr;
   if (fused_crc) {
     const uint32_t total = static_cast<uint32_t>((bs + 4095) / 4096);
     hipError_t te;
@@ -915,25 +1026,17 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
       (void)upload_done(I, u, stream);
       return hip_errno(te);
     }
-    // the partials buffer is reused call to call: a launch on another stream
-    // may still be reading it
-    if (I.crc_part_used && I.crc_part_stream != stream) (void)hipDeviceSynchronize();
     const size_t part_bytes = static_cast<size_t>(n_obj) * total * m * sizeof(uint32_t);
-    if (part_bytes > I.crc_part.cap) {
-      if (I.crc_part_used) (void)hipDeviceSynchronize();
-      if ((e = I.crc_part.ensure(part_bytes)) != hipSuccess) {
-        (void)upload_done(I, u, stream);
-        return hip_errno(e);
-      }
+    if ((e = crc_part_for(I, stream, part_bytes, &crc_part)) != hipSuccess) {
+      (void)upload_done(I, u, stream);
+      return hip_errno(e);
     }
-    I.crc_part_used = true;
-    I.crc_part_stream = stream;
   }
   for (uint32_t p = 0; p < I.passes; ++p) {
     EncodeParams P{};
     P.crc_tables = crc_maps;
     P.crc_finish_tables = crc_fin;
-    P.crc_part = fused_crc ? static_cast<uint32_t*>(I.crc_part.p) : nullptr;
+    P.crc_part = crc_part;
     P.objs = objs;
     P.obj_stride = obj_stride;
     P.obj_len = obj_len;
@@ -1529,6 +1632,12 @@ uint32_t liberasurecode_get_version(void) { return kLibecVersion; }
 uint64_t ecamd_blocksize(int desc, uint64_t obj_len) {
   auto I = lookup(desc);
   return I ? blocksize_of(I->k, I->code.w, obj_len) : 0;
+}
+
+int ecamd_layout_supported(int k, int m, int w, uint64_t obj_len, uint64_t frag_stride,
+                           uint64_t n_obj) {
+  if (k < 1 || m < 1 || k + m > kMaxFragments || (w != 8 && w != 16)) return -EINVALIDPARAMS;
+  return layout_fits(k, m, blocksize_of(k, w, obj_len), frag_stride, n_obj) ? 0 : -EINVALIDPARAMS;
 }
 
 int ecamd_device(int desc) {

@@ -74,16 +74,23 @@ GfMatrix make_generator(int k, int m) {
 }
 
 void build_nibble_tables(const uint16_t* rows, int nrows, int ncols, uint64_t* out) {
+  // Products are GF(2)-linear in the nibble, so entry v is the XOR of the
+  // entries of v's bits: 4 multiplications per (column, position) instead of
+  // 16 (decode builds one set per new erasure pattern, inside the call).
   const Gf16& gf = Gf16::get();
   for (int c = 0; c < ncols; ++c)
-    for (int q = 0; q < 4; ++q)
-      for (int v = 0; v < 16; ++v) {
-        uint64_t e = 0;
-        const uint16_t x = static_cast<uint16_t>(v << (4 * q));
+    for (int q = 0; q < 4; ++q) {
+      uint64_t basis[4] = {0, 0, 0, 0};
+      for (int b = 0; b < 4; ++b) {
+        const uint16_t x = static_cast<uint16_t>(1u << (4 * q + b));
         for (int r = 0; r < nrows && r < 4; ++r)
-          e |= static_cast<uint64_t>(gf.mul(rows[r * ncols + c], x)) << (16 * r);
-        out[c * 64 + (q >> 1) * 32 + v * 2 + (q & 1)] = e;
+          basis[b] |= static_cast<uint64_t>(gf.mul(rows[r * ncols + c], x)) << (16 * r);
       }
+      uint64_t* t = out + c * 64 + (q >> 1) * 32 + (q & 1);
+      for (int v = 0; v < 16; ++v)
+        t[v * 2] = ((v & 1) ? basis[0] : 0) ^ ((v & 2) ? basis[1] : 0) ^ ((v & 4) ? basis[2] : 0) ^
+                   ((v & 8) ? basis[3] : 0);
+    }
 }
 
 }  // namespace ecamd

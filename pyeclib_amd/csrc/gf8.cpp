@@ -83,16 +83,20 @@ bool invert8(const GfMatrix& a, GfMatrix& out, int n) {
 }
 
 void build_nibble_tables8(const uint16_t* rows, int nrows, int ncols, uint32_t* out) {
+  // linear in the nibble: 4 products per (column, position), XOR-combined
   const Gf8& gf = Gf8::get();
   for (int c = 0; c < ncols; ++c)
-    for (int q = 0; q < 2; ++q)
-      for (int v = 0; v < 16; ++v) {
-        uint32_t e = 0;
-        const uint16_t x = static_cast<uint16_t>(v << (4 * q));
+    for (int q = 0; q < 2; ++q) {
+      uint32_t basis[4] = {0, 0, 0, 0};
+      for (int b = 0; b < 4; ++b) {
+        const uint16_t x = static_cast<uint16_t>(1u << (4 * q + b));
         for (int r = 0; r < nrows && r < 4; ++r)
-          e |= static_cast<uint32_t>(gf.mul(rows[r * ncols + c], x)) << (8 * r);
-        out[(c * 2 + q) * 16 + v] = e;
+          basis[b] |= static_cast<uint32_t>(gf.mul(rows[r * ncols + c], x)) << (8 * r);
       }
+      for (int v = 0; v < 16; ++v)
+        out[(c * 2 + q) * 16 + v] = ((v & 1) ? basis[0] : 0) ^ ((v & 2) ? basis[1] : 0) ^
+                                    ((v & 4) ? basis[2] : 0) ^ ((v & 8) ? basis[3] : 0);
+    }
 }
 
 }  // namespace ecamd

@@ -204,3 +204,46 @@ def test_batch_layout_helpers():
     fs = batch.frag_stride(419432)
     assert fs % 128 == 0 and fs >= 80 + 419440
     assert (batch.PAYLOAD_SKEW + 80) % 128 == 0
+
+
+def test_layout_guard_32bit_offsets():
+    """The kernels use 32-bit buffer offsets (object slices below 2^31,
+    stripes below 2^32): layouts past them are refused with -EINVALIDPARAMS
+    instead of wrapping (run_encode / run_decode apply the same
+    check).  Needs no GPU."""
+    from pyeclib_amd import batch
+    f = _native.lib.ecamd_layout_supported
+    bad = -_native.EINVALIDPARAMS
+    L = 4 * 1024 * 1024
+    assert f(10, 4, 16, L, batch.frag_stride(419432), 256) == 0
+    # a 1.9 GiB object still fits; 2 GiB does not (decode's output window)
+    big = 1900 * 2**20
+    assert f(10, 4, 16, big, batch.frag_stride(batch.blocksize(10, big)), 1) == 0
+    assert f(10, 4, 16, 2**31, batch.frag_stride(batch.blocksize(10, 2**31)), 1) == bad
+    # a stripe span (k+m)*frag_stride past 4 GiB
+    assert f(4, 28, 16, 2**30, batch.frag_stride(batch.blocksize(4, 2**30)), 1) == bad
+    # a batch whose 4 KiB work items overflow 31 bits
+    assert f(10, 4, 16, L, batch.frag_stride(419432), 2**25) == bad
+    # bad codes
+    assert f(0, 4, 16, L, 1 << 20, 1) == bad
+    assert f(10, 4, 12, L, 1 << 20, 1) == bad
+
+
+def test_batch_rejects_strided_views():
+    """A fragment group must be packed at k * frag_stride per object: the C
+    API takes only the fragment stride, so a view like stripes[:, :k] is
+    refused rather than read as the wrong bytes."""
+    import torch
+    from pyeclib_amd import batch
+    k, m, fs = 4, 2, 256
+    stripes = torch.zeros((3, k + m, fs), dtype=torch.uint8)
+    chk = batch.BatchCodec._check_rows
+    chk("f", stripes[:, :k])                      # device path: any object stride
+    chk("f", stripes[:, :k].contiguous(), k)      # host path: packed group
+    with pytest.raises(X.ECInvalidParameter):
+        chk("f", stripes[:, :k], k)               # host path: strided group
+    with pytest.raises(X.ECInvalidParameter):
+        chk("f", stripes[:, :, ::2])              # bytes not contiguous
+    with pytest.raises(X.ECInvalidParameter):
+        chk("f", stripes[:, :k + 1].contiguous(), k)  # wrong group size
+    chk("f", stripes[:1, :k], k)                  # one object: stride(0) unused

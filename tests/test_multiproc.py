@@ -2,7 +2,7 @@
 pyeclib_amd.shard, each rank encoding its own range (with the CPU oracle as
 the stand-in codec -- no GPU here), digests gathered and compared with a
 single-process encode of the whole batch; plus the MAX time reduction that
-bench.py uses."""
+bench.py uses (MAX time, MIN verified flag, on CPU tensors: no RCCL)."""
 import hashlib
 import os
 import socket
@@ -44,13 +44,15 @@ def _worker(rank, world, port, n_obj, q):
     gathered = [None] * w
     dist.all_gather_object(gathered, mine)
     t = shard.max_over_ranks(float(rank + 1))
+    ok = shard.min_over_ranks(0 if rank == 1 else 1)
+    total = shard.sum_over_ranks(b - a)
     shard.barrier()
     if rank == 0:
         merged = {}
         for part in gathered:
             merged.update(part)
-        q.put((merged, t))
-    dist.destroy_process_group()
+        q.put((merged, t, ok, total))
+    shard.finish()
 
 
 def test_shard_range_partitions():
@@ -74,10 +76,10 @@ def test_two_rank_gloo_sharded_encode():
     procs = [ctx.Process(target=_worker, args=(r, world, port, n_obj, q)) for r in range(world)]
     for p in procs:
         p.start()
-    merged, tmax = q.get(timeout=120)
+    merged, tmax, ok, total = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     objs = _objects(n_obj, 3000)
     assert merged == {i: _digest(O.encode(4, 2, objs[i])) for i in range(n_obj)}
-    assert tmax == 2.0
+    assert tmax == 2.0 and ok == 0 and total == n_obj

@@ -22,12 +22,33 @@ for s in $STEPS; do
     (cd $R && timeout -k 10 600 python3 -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 300 \
         --timeout-method thread > $O/pytest_gpu_new.log 2>&1)
     tail -3 $O/pytest_gpu_new.log ;;
+  membench)
+    (cd $R && timeout -k 10 300 tools/membench ${MB_REPS:-20} ${MB_SECTIONS:-} > $O/membench.txt 2>&1)
+    cat $O/membench.txt ;;
+  multirank)
+    (cd $R && timeout -k 10 600 python3 -u -m pytest tests/test_gpu_multirank.py -m gpu -x -v --timeout 300 \
+        --timeout-method thread > $O/pytest_multirank.log 2>&1)
+    tail -3 $O/pytest_multirank.log ;;
+  config0)
+    (cd $R && timeout -k 10 400 python3 bench.py --no-host --no-cpu-baseline --config0 --steps 5 \
+        > $O/config0_bench.json 2> $O/config0_bench.err)
+    tail -c 900 $O/config0_bench.json ;;
+  sysfs)
+    (ls /sys/class/kfd/kfd/topology/nodes/; for n in /sys/class/kfd/kfd/topology/nodes/*; do \
+      echo "== $n"; grep -E "simd_count|location_id|domain|drm_render_minor" $n/properties; done; \
+      echo "== numa"; for d in /sys/class/drm/card*/device; do echo "$d $(cat $d/numa_node 2>/dev/null)"; done; \
+      cat /sys/devices/system/node/node*/cpulist; nproc; python3 -c "import os; print(len(os.sched_getaffinity(0)))"; \
+      echo "ROCR=$ROCR_VISIBLE_DEVICES HIP=$HIP_VISIBLE_DEVICES CUDA=$CUDA_VISIBLE_DEVICES") > $O/sysfs.txt 2>&1 || true
+    cat $O/sysfs.txt ;;
   smoke)
     (cd $R && timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1)
     tail -1 $O/smoke.log ;;
   ab)
     (cd $R && timeout -k 10 400 python3 tools/ab_bench.py ${AB:-base ECAMD_DEC_OCC3=1 ECAMD_XCD=0} > $O/ab.txt 2>&1)
     cat $O/ab.txt ;;
+  abfull)
+    (cd $R && timeout -k 10 400 python3 tools/ab_bench.py --full-stripe ${ABF:-base ECAMD_DATA_COPY=1} > $O/ab_full.txt 2>&1)
+    cat $O/ab_full.txt ;;
   single)
     (cd $R && timeout -k 10 300 python3 tools/single_ab.py > $O/single_ab.txt 2>&1)
     cat $O/single_ab.txt ;;

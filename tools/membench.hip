@@ -10,12 +10,18 @@
 // bs is a runtime argument, so bs = 419432 (the real, 8-mod-16 slices) and
 // bs = 419456 (128-B-aligned slices) isolate the misalignment cost.
 //
-//   ./membench [reps]
+// Every shape is checked on the host against the buffers it touches before
+// its first launch (round 2's compact-layout probe overran the fragment
+// buffer by 2.85 MB: its stripes were sized for a different object count).
+//
+//   ./membench [reps] [sections]     sections: any of "base enc dec alt" (default all)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <algorithm>
 #include <vector>
 
 #define CHECK(x)                                                               \
@@ -53,6 +59,61 @@ struct Shape {
 
 constexpr int K = 10, M = 4;
 
+// Host-side bounds check of one shape against its buffers: tile span T bytes
+// of payload positions per item (4096 * CH).  Exits on a violation.
+struct Bufs {
+  uint8_t *objs_base, *out_base, *frags_base;
+  uint64_t obj_bytes, frag_bytes;
+};
+Bufs g_bufs;
+void check_shape(const char* name, const Shape& s, uint64_t span, bool in_out = false) {
+  const uint64_t obj_end = (s.objs - (in_out ? g_bufs.out_base : g_bufs.objs_base)) +
+                           uint64_t(s.n_obj - 1) * s.obj_stride + uint64_t(K - 1) * s.bs +
+                           uint64_t(s.tiles) * span;
+  const uint64_t frag_end = (s.frags - g_bufs.frags_base) + uint64_t(s.n_obj - 1) * s.stripe_stride +
+                            uint64_t(K + M - 1) * s.frag_stride + 80 + uint64_t(s.tiles) * span;
+  const bool obj_ok = obj_end <= g_bufs.obj_bytes;
+  const bool frag_ok = frag_end <= g_bufs.frag_bytes;
+  if (!obj_ok || !frag_ok || uint64_t(s.tiles) * span > s.bs + 0ull) {
+    std::fprintf(stderr, "shape %s out of bounds: obj end %llu / %llu, frag end %llu / %llu, "
+                 "tile span %llu vs bs %u\n", name, (unsigned long long)obj_end,
+                 (unsigned long long)g_bufs.obj_bytes, (unsigned long long)frag_end,
+                 (unsigned long long)g_bufs.frag_bytes,
+                 (unsigned long long)(uint64_t(s.tiles) * span), s.bs);
+    std::exit(2);
+  }
+}
+
+// Item order (item w = object w / tiles, tile w % tiles).
+//   0 PLAIN: grid-stride over the item list.
+//   1 XCD: the list cut into 8 contiguous ranges, range x walked by the blocks
+//     with b % 8 == x (blocks are dealt round-robin over the 8 XCDs).
+//   2 OBJECT: P = grid / n_obj blocks per object; block b takes object
+//     b % n_obj, tiles c, c + P, c + 2P, ... (c = b / n_obj): every object
+//     in flight at once, each block's items one fixed stride apart inside
+//     one object (what a per-thread Horner CRC over the parity needs).
+//   3 RANGE: block b takes the contiguous items [n b / G, n (b+1) / G)
+//     (the fused-CRC encode's order).
+struct Order {
+  uint32_t begin, end, step;
+};
+template <int ORD>
+__device__ __forceinline__ Order order(uint32_t items, uint32_t tiles = 1) {
+  if constexpr (ORD == 0) return {blockIdx.x, items, gridDim.x};
+  if constexpr (ORD == 1) {
+    const uint32_t x = blockIdx.x & 7u;
+    const uint32_t lo = uint32_t(uint64_t(items) * x / 8), hi = uint32_t(uint64_t(items) * (x + 1) / 8);
+    return {lo + (blockIdx.x >> 3), hi, gridDim.x >> 3};
+  }
+  if constexpr (ORD == 2) {
+    const uint32_t n_obj = items / tiles, per = gridDim.x / n_obj;  // host: grid % n_obj == 0
+    const uint32_t o = blockIdx.x % n_obj, c = blockIdx.x / n_obj;
+    return {o * tiles + c, o * tiles + tiles, per};
+  }
+  return {uint32_t(uint64_t(items) * blockIdx.x / gridDim.x),
+          uint32_t(uint64_t(items) * (blockIdx.x + 1) / gridDim.x), 1u};
+}
+
 // ---- plain copy / read sweeps (grid-stride, 16 B per lane, CH units per lane
 // per step, each unit one contiguous 1 KiB wave access) ----
 template <int CH, bool NT>
@@ -83,11 +144,23 @@ __global__ void __launch_bounds__(256) read_kernel(const uint8_t* src, uint64_t 
   }
   if (acc == 0x12345678u) sink[0] = acc;
 }
+template <int CH, bool NT>
+__global__ void __launch_bounds__(256) write_kernel(uint8_t* dst, uint64_t n) {
+  const uint64_t step = uint64_t(gridDim.x) * 256 * 16 * CH;
+  const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint64_t b = uint64_t(blockIdx.x) * 256 * 16 * CH + wave * 1024 * CH + lane * 16; b < n;
+       b += step) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) st<NT>(dst + b + 1024 * c, v4u{uint32_t(b), 1u, 2u, 3u});
+  }
+}
 
 // ---- encode stream: item = (object, tile of 4096*CH payload positions);
 // wave w of the block takes [x, x + 1024*CH) with x = tile*4096*CH + w*1024*CH.
-// PF: the block's next item is loaded before this one is consumed. ----
-template <int CH, bool NTL, bool NTS>
+// PF: the block's next item is loaded before this one is consumed.
+// SROW: parity stored row-major (each row's CH KiB back to back: a store
+// burst of CH KiB per row) instead of chunk-major. ----
+template <int CH, bool NTL>
 __device__ __forceinline__ void enc_load(const Shape& s, uint32_t w, v4u (&v)[K][CH]) {
   const uint32_t o = w / s.tiles, t = w - o * s.tiles;
   const uint32_t x = t * 4096 * CH + (threadIdx.x >> 6) * 1024 * CH + (threadIdx.x & 63) * 16;
@@ -97,21 +170,28 @@ __device__ __forceinline__ void enc_load(const Shape& s, uint32_t w, v4u (&v)[K]
 #pragma unroll
     for (int c = 0; c < CH; ++c) v[j][c] = ld<NTL>(src + uint64_t(j) * s.bs + 1024 * c);
 }
-template <int CH, bool NTL, bool NTS>
+template <int CH, bool NTS, bool SROW>
 __device__ __forceinline__ void enc_store(const Shape& s, uint32_t w, const v4u (&v)[K][CH]) {
   const uint32_t o = w / s.tiles, t = w - o * s.tiles;
   const uint32_t x = t * 4096 * CH + (threadIdx.x >> 6) * 1024 * CH + (threadIdx.x & 63) * 16;
   uint8_t* dst = s.frags + o * s.stripe_stride + K * s.frag_stride + 80 + x;
+  v4u a[CH];
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
-    v4u a = v[0][c];
+    a[c] = v[0][c];
 #pragma unroll
-    for (int j = 1; j < K; ++j) a ^= v[j][c];
+    for (int j = 1; j < K; ++j) a[c] ^= v[j][c];
+  }
+  if constexpr (SROW) {
 #pragma unroll
-    for (int r = 0; r < M; ++r) {
-      st<NTS>(dst + r * s.frag_stride + 1024 * c, a);
-      a.x += 1;
-    }
+    for (int r = 0; r < M; ++r)
+#pragma unroll
+      for (int c = 0; c < CH; ++c) st<NTS>(dst + r * s.frag_stride + 1024 * c, a[c] + uint32_t(r));
+  } else {
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+#pragma unroll
+      for (int r = 0; r < M; ++r) st<NTS>(dst + r * s.frag_stride + 1024 * c, a[c] + uint32_t(r));
   }
 }
 // MODE 1: loads only (XOR folded into a never-taken store), MODE 2: stores only
@@ -122,44 +202,153 @@ __global__ void __launch_bounds__(256) enc_half_kernel(Shape s, uint32_t* sink) 
   for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
     v4u v[K][1];
     if constexpr (MODE == 1) {
-      enc_load<1, NTL, true>(s, w, v);
+      enc_load<1, NTL>(s, w, v);
 #pragma unroll
       for (int j = 0; j < K; ++j) acc ^= v[j][0].x ^ v[j][0].y ^ v[j][0].z ^ v[j][0].w;
     } else {
 #pragma unroll
       for (int j = 0; j < K; ++j) v[j][0] = v4u{w, uint32_t(j), 0u, 1u};
-      enc_store<1, NTL, true>(s, w, v);
+      enc_store<1, true, false>(s, w, v);
     }
   }
   if (acc == 0x12345678u) sink[0] = acc;
 }
 
-template <int CH, bool NTL, bool NTS, bool PF>
+template <int CH, bool NTL, bool NTS, bool PF, int ORD = 0, bool SROW = false>
 __global__ void __launch_bounds__(256) enc_kernel(Shape s) {
-  const uint32_t items = s.n_obj * s.tiles;
+  const Order r = order<ORD>(s.n_obj * s.tiles, s.tiles);
   if constexpr (!PF) {
-    for (uint32_t w = blockIdx.x; w < items; w += gridDim.x) {
+    for (uint32_t w = r.begin; w < r.end; w += r.step) {
       v4u v[K][CH];
-      enc_load<CH, NTL, NTS>(s, w, v);
-      enc_store<CH, NTL, NTS>(s, w, v);
+      enc_load<CH, NTL>(s, w, v);
+      enc_store<CH, NTS, SROW>(s, w, v);
     }
   } else {
-    uint32_t w = blockIdx.x;
-    if (w >= items) return;
+    uint32_t w = r.begin;
+    if (w >= r.end) return;
     v4u a[K][CH], b[K][CH];
-    enc_load<CH, NTL, NTS>(s, w, a);
+    enc_load<CH, NTL>(s, w, a);
     while (true) {
-      uint32_t wn = w + gridDim.x < items ? w + gridDim.x : w;
-      enc_load<CH, NTL, NTS>(s, wn, b);
-      enc_store<CH, NTL, NTS>(s, w, a);
+      uint32_t wn = w + r.step < r.end ? w + r.step : w;
+      enc_load<CH, NTL>(s, wn, b);
+      enc_store<CH, NTS, SROW>(s, w, a);
       if (wn == w) break;
       w = wn;
-      wn = w + gridDim.x < items ? w + gridDim.x : w;
-      enc_load<CH, NTL, NTS>(s, wn, a);
-      enc_store<CH, NTL, NTS>(s, w, b);
+      wn = w + r.step < r.end ? w + r.step : w;
+      enc_load<CH, NTL>(s, wn, a);
+      enc_store<CH, NTS, SROW>(s, w, b);
       if (wn == w) break;
       w = wn;
     }
+  }
+}
+
+// The product kernel's stream shape without the lookups: NB input chunks in
+// flight per wave, refilled as each is consumed, running over into the
+// block's next item (ec_kernels_impl.hpp encode_interior).  CH chunks per
+// wave per item, consumed chunk-major (all K inputs of chunk c, then c + 1).
+template <int CH, int NB, int ORD>
+__global__ void __launch_bounds__(256) enc_stream_kernel(Shape s) {
+  constexpr int SL = K * CH;  // slots per item
+  const Order r = order<ORD>(s.n_obj * s.tiles, s.tiles);
+  uint32_t w = r.begin;
+  if (w >= r.end) return;
+  const uint32_t lanex = (threadIdx.x >> 6) * 1024 * CH + (threadIdx.x & 63) * 16;
+  auto src_of = [&](uint32_t it, int slot) {
+    const uint32_t o = it / s.tiles, t = it - o * s.tiles;
+    const int c = slot / K, j = slot % K;
+    return s.objs + o * s.obj_stride + uint64_t(j) * s.bs + t * 4096 * CH + lanex + 1024 * c;
+  };
+  v4u buf[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) buf[i] = ld<false>(src_of(w, i));
+  while (true) {
+    const uint32_t wn = w + r.step < r.end ? w + r.step : w;
+    const uint32_t o = w / s.tiles, t = w - o * s.tiles;
+    uint8_t* dst = s.frags + o * s.stripe_stride + K * s.frag_stride + 80 + t * 4096 * CH + lanex;
+    v4u acc = v4u{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < SL; ++i) {
+      acc ^= buf[i % NB];
+      if (i + NB < SL)
+        buf[i % NB] = ld<false>(src_of(w, i + NB));
+      else if (wn != w)
+        buf[i % NB] = ld<false>(src_of(wn, i + NB - SL));
+      if (i % K == K - 1) {
+#pragma unroll
+        for (int q = 0; q < M; ++q) st<true>(dst + q * s.frag_stride + 1024 * (i / K), acc + uint32_t(q));
+        acc = v4u{0u, 0u, 0u, 0u};
+      }
+    }
+    if (wn == w) break;
+    w = wn;
+  }
+}
+
+// The same stream through buffer instructions, as the product kernels issue
+// them (ec_kernels_impl.hpp: one wave-uniform descriptor per object, the
+// lane's 16*lane in voffset, every per-input / per-row offset in soffset).
+// NTL: nontemporal loads; ST_NOP: the product's one wait state after each
+// 16-B store.
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc mk_rsrc(const void* base, int records = -1) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  const int n = static_cast<int>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(records)));
+  return __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, n, 0x00020000);
+}
+template <int CH, int NB, int ORD, bool NTL, bool ST_NOP>
+__global__ void __launch_bounds__(256) enc_stream_buf_kernel(Shape s) {
+  constexpr int SL = K * CH;  // slots per item
+  const Order r = order<ORD>(s.n_obj * s.tiles, s.tiles);
+  uint32_t w = r.begin;
+  if (w >= r.end) return;
+  const uint32_t lane16 = (threadIdx.x & 63) * 16;
+  const uint32_t wx = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * 1024 * CH);
+  auto item_x = [&](uint32_t it) { return (it - it / s.tiles * s.tiles) * 4096 * CH + wx; };
+  auto obj_of = [&](uint32_t it, int rec) { return mk_rsrc(s.objs + (it / s.tiles) * s.obj_stride, rec); };
+  Rsrc cur = obj_of(w, -1);
+  uint32_t x = item_x(w);
+  v4u buf[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+    buf[i] = __builtin_amdgcn_raw_buffer_load_b128(cur, lane16, (i % K) * s.bs + x + 1024 * (i / K),
+                                                  NTL ? 2 : 0);
+  while (true) {
+    const uint32_t wn = w + r.step < r.end ? w + r.step : w;
+    const Rsrc nxt = obj_of(wn, wn == w ? 0 : -1);
+    const uint32_t xn = item_x(wn);
+    const Rsrc par = mk_rsrc(s.frags + (w / s.tiles) * s.stripe_stride);
+    v4u acc = v4u{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < SL; ++i) {
+      acc ^= buf[i % NB];
+      if (i + NB < SL)
+        buf[i % NB] = __builtin_amdgcn_raw_buffer_load_b128(
+            cur, lane16, ((i + NB) % K) * s.bs + x + 1024 * ((i + NB) / K), NTL ? 2 : 0);
+      else
+        buf[i % NB] = __builtin_amdgcn_raw_buffer_load_b128(
+            nxt, lane16, ((i + NB - SL) % K) * s.bs + xn + 1024 * ((i + NB - SL) / K), NTL ? 2 : 0);
+      if (i % K == K - 1) {
+#pragma unroll
+        for (int q = 0; q < M; ++q) {
+          __builtin_amdgcn_raw_buffer_store_b128(acc + uint32_t(q), par, lane16,
+                                                 uint32_t(K + q) * uint32_t(s.frag_stride) + 80 + x + 1024 * (i / K), 2);
+          if constexpr (ST_NOP) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_nop 0");
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        acc = v4u{0u, 0u, 0u, 0u};
+      }
+    }
+    if (wn == w) break;
+    w = wn;
+    x = xn;
+    cur = nxt;
   }
 }
 
@@ -192,6 +381,7 @@ double time_us(F launch) {
   launch();
   launch();
   CHECK(hipDeviceSynchronize());
+  CHECK(hipGetLastError());
   CHECK(hipEventRecord(e0, 0));
   for (int i = 0; i < g_reps; ++i) launch();
   CHECK(hipEventRecord(e1, 0));
@@ -199,18 +389,52 @@ double time_us(F launch) {
   float ms = 0;
   CHECK(hipEventElapsedTime(&ms, e0, e1));
   CHECK(hipGetLastError());
+  CHECK(hipEventDestroy(e0));
+  CHECK(hipEventDestroy(e1));
   return ms * 1e3 / g_reps;
 }
 
+// Alternating form (bench.py's step): `other` then `timed`, g_reps times;
+// the mean time of `timed` alone, from events around it.
+template <typename A, typename B>
+double time_alt_us(A other, B timed) {
+  std::vector<hipEvent_t> ev(2 * g_reps);
+  for (auto& e : ev) CHECK(hipEventCreate(&e));
+  other();
+  timed();
+  CHECK(hipDeviceSynchronize());
+  for (int i = 0; i < g_reps; ++i) {
+    other();
+    CHECK(hipEventRecord(ev[2 * i], 0));
+    timed();
+    CHECK(hipEventRecord(ev[2 * i + 1], 0));
+  }
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipGetLastError());
+  double sum = 0;
+  for (int i = 0; i < g_reps; ++i) {
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
+    sum += ms;
+  }
+  for (auto& e : ev) CHECK(hipEventDestroy(e));
+  return sum * 1e3 / g_reps;
+}
+
 void report(const char* name, int bpc, double us, double bytes) {
-  std::printf("%-44s bpc=%d %9.1f us %8.1f GB/s\n", name, bpc, us, bytes / us / 1e3);
+  std::printf("%-52s bpc=%d %9.1f us %8.1f GB/s\n", name, bpc, us, bytes / us / 1e3);
   std::fflush(stdout);
+}
+
+bool want(const char* sections, const char* s) {
+  return sections == nullptr || std::strstr(sections, s) != nullptr;
 }
 
 }  // namespace
 
 int main(int argc, char** argv) {
   if (argc > 1) g_reps = std::atoi(argv[1]);
+  const char* sections = argc > 2 ? argv[2] : nullptr;
   int dev = 0;
   CHECK(hipGetDevice(&dev));
   CHECK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -220,8 +444,13 @@ int main(int argc, char** argv) {
   const uint64_t obj_stride = L;
   const uint64_t fs = ((80 + (bs_al + 15) / 16 * 16) + 127) / 128 * 128;
   const uint64_t ss = fs * (K + M);
+  // compact layout: many small objects holding the same bytes (10 slices of
+  // 40 KiB), stripes of 14 fragments of 40 KiB + 128
+  const uint32_t sbs = 40960, sobj = 10 * sbs, sfs = sbs + 128;
+  const uint64_t sss = uint64_t(sfs) * (K + M);
+  const uint32_t n_compact = uint32_t(uint64_t(n_obj) * obj_stride / sobj);
   const uint64_t obj_bytes = obj_stride * n_obj + (1 << 20);
-  const uint64_t frag_bytes = ss * n_obj + (1 << 20);
+  const uint64_t frag_bytes = std::max(ss * n_obj, sss * n_compact) + (1 << 20);
   uint8_t *objs, *frags_raw, *out;
   uint32_t* sink;
   CHECK(hipMalloc(&objs, obj_bytes));
@@ -232,71 +461,150 @@ int main(int argc, char** argv) {
   CHECK(hipMemset(out, 0, obj_bytes));
   CHECK(hipMemset(frags_raw, 2, frag_bytes));
   uint8_t* frags = frags_raw + 48;  // payloads (80 B past each fragment start) 128-B aligned
+  g_bufs = {objs, out, frags_raw, obj_bytes, frag_bytes};
   std::printf("CUs %d, reps %d, bs %u / aligned %u, frag_stride %llu\n", g_cus, g_reps, bs_real,
               bs_al, (unsigned long long)fs);
 
   const uint64_t n_copy = uint64_t(n_obj) * L;
-  for (int bpc : {2, 4, 8}) {
-    const int grid = g_cus * bpc;
-    report("copy 1 GiB, 16 B/lane, cached", bpc,
-           time_us([&] { copy_kernel<1, false><<<grid, 256>>>(objs, out, n_copy); }), 2.0 * n_copy);
-    report("copy 1 GiB, 16 B/lane, nt", bpc,
-           time_us([&] { copy_kernel<1, true><<<grid, 256>>>(objs, out, n_copy); }), 2.0 * n_copy);
-    report("copy 1 GiB, 2x16 B/lane, nt", bpc,
-           time_us([&] { copy_kernel<2, true><<<grid, 256>>>(objs, out, n_copy); }), 2.0 * n_copy);
-    report("read 1 GiB, 16 B/lane, nt", bpc,
-           time_us([&] { read_kernel<1, true><<<grid, 256>>>(objs, n_copy, sink); }), 1.0 * n_copy);
-    report("read 1 GiB, 4x16 B/lane, cached", bpc,
-           time_us([&] { read_kernel<4, false><<<grid, 256>>>(objs, n_copy, sink); }), 1.0 * n_copy);
+  if (want(sections, "base")) {
+    for (int bpc : {2, 4, 8}) {
+      const int grid = g_cus * bpc;
+      report("copy 1 GiB, 16 B/lane, nt", bpc,
+             time_us([&] { copy_kernel<1, true><<<grid, 256>>>(objs, out, n_copy); }), 2.0 * n_copy);
+      report("copy 1 GiB, 2x16 B/lane, nt", bpc,
+             time_us([&] { copy_kernel<2, true><<<grid, 256>>>(objs, out, n_copy); }), 2.0 * n_copy);
+      report("read 1 GiB, 16 B/lane, cached", bpc,
+             time_us([&] { read_kernel<1, false><<<grid, 256>>>(objs, n_copy, sink); }), 1.0 * n_copy);
+      report("read 1 GiB, 4x16 B/lane, cached", bpc,
+             time_us([&] { read_kernel<4, false><<<grid, 256>>>(objs, n_copy, sink); }), 1.0 * n_copy);
+      report("write 1 GiB, 16 B/lane, nt", bpc,
+             time_us([&] { write_kernel<1, true><<<grid, 256>>>(out, n_copy); }), 1.0 * n_copy);
+    }
   }
-  {
-    // split the 10:4 encode mix into its halves, and a compact layout (many
-    // small objects: 10 slices of 40 KiB, same bytes) to test page locality
-    Shape s{objs, frags, bs_real, n_obj, bs_real / 4096, obj_stride, fs, ss};
-    double rb = double(n_obj) * s.tiles * 4096 * K, wb = double(n_obj) * s.tiles * 4096 * M;
+  Shape s{objs, frags, bs_real, n_obj, bs_real / 4096, obj_stride, fs, ss};
+  const double enc_bytes = double(n_obj) * s.tiles * 4096 * (K + M);
+  if (want(sections, "enc")) {
+    // the 10:4 encode mix split into its halves
+    check_shape("enc halves", s, 4096);
+    const double rb = double(n_obj) * s.tiles * 4096 * K, wb = double(n_obj) * s.tiles * 4096 * M;
     for (int bpc : {4, 8}) {
       const int grid = g_cus * bpc;
       report("enc reads only, cached", bpc, time_us([&] { enc_half_kernel<false, 1><<<grid, 256>>>(s, sink); }), rb);
-      report("enc reads only, nt", bpc, time_us([&] { enc_half_kernel<true, 1><<<grid, 256>>>(s, sink); }), rb);
       report("enc writes only, nt", bpc, time_us([&] { enc_half_kernel<true, 2><<<grid, 256>>>(s, sink); }), wb);
-      const uint32_t sbs = 40960, sobj = 10 * sbs, sfs = sbs + 128;
-      Shape c{objs, frags, sbs, uint32_t(uint64_t(n_obj) * obj_stride / sobj), sbs / 4096, sobj, sfs, uint64_t(sfs) * (K + M)};
-      const double cb = double(c.n_obj) * c.tiles * 4096 * (K + M);
-      report("enc compact 40 KiB slices, ld-cached st-nt PF", bpc,
-             time_us([&] { enc_kernel<1, false, true, true><<<grid, 256>>>(c); }), cb);
     }
-  }
-  for (uint32_t bs : {bs_real, bs_al}) {
-    Shape s{objs, frags, bs, n_obj, 0, obj_stride, fs, ss};
-    const bool al = bs == bs_al;
-    char name[128];
+    // compact layout (page-locality probe)
+    Shape c{objs, frags, sbs, n_compact, sbs / 4096, sobj, sfs, sss};
+    check_shape("enc compact", c, 4096);
+    const double cb = double(c.n_obj) * c.tiles * 4096 * (K + M);
     for (int bpc : {2, 4, 8}) {
       const int grid = g_cus * bpc;
-      s.tiles = bs_real / 4096;
-      double bytes = double(n_obj) * s.tiles * 4096 * (K + M);
-      std::snprintf(name, sizeof name, "enc %s ld-cached st-nt", al ? "aligned" : "real   ");
-      report(name, bpc, time_us([&] { enc_kernel<1, false, true, false><<<grid, 256>>>(s); }), bytes);
-      std::snprintf(name, sizeof name, "enc %s ld-cached st-nt PF", al ? "aligned" : "real   ");
-      report(name, bpc, time_us([&] { enc_kernel<1, false, true, true><<<grid, 256>>>(s); }), bytes);
-      std::snprintf(name, sizeof name, "enc %s ld-nt st-nt PF", al ? "aligned" : "real   ");
-      report(name, bpc, time_us([&] { enc_kernel<1, true, true, true><<<grid, 256>>>(s); }), bytes);
-      std::snprintf(name, sizeof name, "enc %s ld-cached st-cached PF", al ? "aligned" : "real   ");
-      report(name, bpc, time_us([&] { enc_kernel<1, false, false, true><<<grid, 256>>>(s); }), bytes);
-      s.tiles = bs_real / 8192;
-      bytes = double(n_obj) * s.tiles * 8192 * (K + M);
-      std::snprintf(name, sizeof name, "enc %s ld-cached st-nt CH2", al ? "aligned" : "real   ");
-      report(name, bpc, time_us([&] { enc_kernel<2, false, true, false><<<grid, 256>>>(s); }), bytes);
-      s.tiles = bs_real / 4096;
-      bytes = double(n_obj) * s.tiles * 4096 * (2 * K);
-      std::snprintf(name, sizeof name, "dec %s ld-nt st-nt", al ? "aligned" : "real   ");
-      Shape d = s;
-      d.objs = out;
-      report(name, bpc, time_us([&] { dec_kernel<true, true><<<grid, 256>>>(d); }), bytes);
-      std::snprintf(name, sizeof name, "dec %s ld-nt st-cached", al ? "aligned" : "real   ");
-      report(name, bpc, time_us([&] { dec_kernel<true, false><<<grid, 256>>>(d); }), bytes);
-      std::snprintf(name, sizeof name, "dec %s ld-cached st-cached", al ? "aligned" : "real   ");
-      report(name, bpc, time_us([&] { dec_kernel<false, false><<<grid, 256>>>(d); }), bytes);
+      report("enc compact 40 KiB slices, CH1", bpc,
+             time_us([&] { enc_kernel<1, false, true, false><<<grid, 256>>>(c); }), cb);
+      report("enc compact 40 KiB slices, CH1 PF", bpc,
+             time_us([&] { enc_kernel<1, false, true, true><<<grid, 256>>>(c); }), cb);
+    }
+    // chunk width per wave (CH KiB of every slice), order, store burst
+    for (int bpc : {1, 2, 4, 8}) {
+      const int grid = g_cus * bpc;
+      Shape s1 = s, s2 = s, s4 = s;
+      s2.tiles = bs_real / 8192;
+      s4.tiles = bs_real / 16384;
+      check_shape("CH1", s1, 4096);
+      check_shape("CH2", s2, 8192);
+      check_shape("CH4", s4, 16384);
+      const double b1 = double(n_obj) * s1.tiles * 4096 * (K + M);
+      const double b2 = double(n_obj) * s2.tiles * 8192 * (K + M);
+      const double b4 = double(n_obj) * s4.tiles * 16384 * (K + M);
+      report("enc CH1", bpc, time_us([&] { enc_kernel<1, false, true, false><<<grid, 256>>>(s1); }), b1);
+      report("enc CH1 xcd", bpc, time_us([&] { enc_kernel<1, false, true, false, 1><<<grid, 256>>>(s1); }), b1);
+      report("enc CH1 object-major", bpc, time_us([&] { enc_kernel<1, false, true, false, 2><<<grid, 256>>>(s1); }), b1);
+      report("enc CH1 block ranges", bpc, time_us([&] { enc_kernel<1, false, true, false, 3><<<grid, 256>>>(s1); }), b1);
+      report("enc CH1 PF", bpc, time_us([&] { enc_kernel<1, false, true, true><<<grid, 256>>>(s1); }), b1);
+      report("enc CH2", bpc, time_us([&] { enc_kernel<2, false, true, false><<<grid, 256>>>(s2); }), b2);
+      report("enc CH2 xcd", bpc, time_us([&] { enc_kernel<2, false, true, false, 1><<<grid, 256>>>(s2); }), b2);
+      report("enc CH2 object-major", bpc, time_us([&] { enc_kernel<2, false, true, false, 2><<<grid, 256>>>(s2); }), b2);
+      report("enc CH2 row-burst stores", bpc,
+             time_us([&] { enc_kernel<2, false, true, false, 0, true><<<grid, 256>>>(s2); }), b2);
+      report("enc CH2 ld-nt", bpc, time_us([&] { enc_kernel<2, true, true, false><<<grid, 256>>>(s2); }), b2);
+      if (bpc <= 4) {
+        report("enc CH2 PF", bpc, time_us([&] { enc_kernel<2, false, true, true><<<grid, 256>>>(s2); }), b2);
+        report("enc CH4", bpc, time_us([&] { enc_kernel<4, false, true, false><<<grid, 256>>>(s4); }), b4);
+        report("enc CH4 row-burst stores", bpc,
+               time_us([&] { enc_kernel<4, false, true, false, 0, true><<<grid, 256>>>(s4); }), b4);
+      }
+      // the product kernel's stream shape
+      report("enc stream CH1 NB5", bpc, time_us([&] { enc_stream_kernel<1, 5, 0><<<grid, 256>>>(s1); }), b1);
+      report("enc stream CH1 NB5 xcd", bpc, time_us([&] { enc_stream_kernel<1, 5, 1><<<grid, 256>>>(s1); }), b1);
+      report("enc stream CH1 NB5 object-major", bpc, time_us([&] { enc_stream_kernel<1, 5, 2><<<grid, 256>>>(s1); }), b1);
+      report("enc stream CH1 NB5 block ranges", bpc, time_us([&] { enc_stream_kernel<1, 5, 3><<<grid, 256>>>(s1); }), b1);
+      report("enc stream CH1 NB10", bpc, time_us([&] { enc_stream_kernel<1, 10, 0><<<grid, 256>>>(s1); }), b1);
+      report("enc buf-stream CH1 NB5 xcd (product)", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 5, 1, false, true><<<grid, 256>>>(s1); }), b1);
+      report("enc buf-stream CH1 NB5 xcd no-nop", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 5, 1, false, false><<<grid, 256>>>(s1); }), b1);
+      report("enc buf-stream CH1 NB5 plain", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 5, 0, false, true><<<grid, 256>>>(s1); }), b1);
+      report("enc buf-stream CH1 NB5 xcd ld-nt", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 5, 1, true, true><<<grid, 256>>>(s1); }), b1);
+      report("enc buf-stream CH2 NB5 xcd ld-nt", bpc,
+             time_us([&] { enc_stream_buf_kernel<2, 5, 1, true, true><<<grid, 256>>>(s2); }), b2);
+      report("enc buf-stream CH2 NB10 xcd ld-nt", bpc,
+             time_us([&] { enc_stream_buf_kernel<2, 10, 1, true, true><<<grid, 256>>>(s2); }), b2);
+      report("enc buf-stream CH2 NB10 plain ld-nt", bpc,
+             time_us([&] { enc_stream_buf_kernel<2, 10, 0, true, true><<<grid, 256>>>(s2); }), b2);
+      report("enc stream CH2 NB5", bpc, time_us([&] { enc_stream_kernel<2, 5, 0><<<grid, 256>>>(s2); }), b2);
+      report("enc stream CH2 NB10", bpc, time_us([&] { enc_stream_kernel<2, 10, 0><<<grid, 256>>>(s2); }), b2);
+      report("enc stream CH4 NB10", bpc, time_us([&] { enc_stream_kernel<4, 10, 0><<<grid, 256>>>(s4); }), b4);
+    }
+    // aligned slices (isolates the 8-mod-16 slice misalignment)
+    Shape a = s;
+    a.bs = bs_al;
+    check_shape("enc aligned", a, 4096);
+    for (int bpc : {2, 8}) {
+      const int grid = g_cus * bpc;
+      report("enc aligned CH1", bpc, time_us([&] { enc_kernel<1, false, true, false><<<grid, 256>>>(a); }), enc_bytes);
+      Shape a2 = a;
+      a2.tiles = bs_real / 8192;
+      report("enc aligned CH2", bpc, time_us([&] { enc_kernel<2, false, true, false><<<grid, 256>>>(a2); }),
+             double(n_obj) * a2.tiles * 8192 * (K + M));
     }
   }
+  if (want(sections, "dec")) {
+    for (uint32_t bs : {bs_real, bs_al}) {
+      Shape d{out, frags, bs, n_obj, bs_real / 4096, obj_stride, fs, ss};
+      check_shape("dec", d, 4096, true);
+      const double bytes = double(n_obj) * d.tiles * 4096 * (2 * K);
+      for (int bpc : {2, 4, 8}) {
+        const int grid = g_cus * bpc;
+        report(bs == bs_al ? "dec aligned ld-nt st-nt" : "dec real    ld-nt st-nt", bpc,
+               time_us([&] { dec_kernel<true, true><<<grid, 256>>>(d); }), bytes);
+      }
+    }
+  }
+  if (want(sections, "alt")) {
+    // bench.py's alternating step: encode after a decode pattern (and vice
+    // versa), each timed alone with events around it
+    Shape d{out, frags, bs_real, n_obj, bs_real / 4096, obj_stride, fs, ss};
+    Shape s2 = s;
+    s2.tiles = bs_real / 8192;
+    const double dec_bytes = double(n_obj) * d.tiles * 4096 * (2 * K);
+    const int g8 = g_cus * 8, g2 = g_cus * 2;
+    report("alt: enc CH1 after dec", 8,
+           time_alt_us([&] { dec_kernel<true, true><<<g2, 256>>>(d); },
+                       [&] { enc_kernel<1, false, true, false><<<g8, 256>>>(s); }), enc_bytes);
+    report("alt: enc CH2 after dec", 2,
+           time_alt_us([&] { dec_kernel<true, true><<<g2, 256>>>(d); },
+                       [&] { enc_kernel<2, false, true, false><<<g2, 256>>>(s2); }),
+           double(n_obj) * s2.tiles * 8192 * (K + M));
+    report("alt: dec after enc CH1", 2,
+           time_alt_us([&] { enc_kernel<1, false, true, false><<<g8, 256>>>(s); },
+                       [&] { dec_kernel<true, true><<<g2, 256>>>(d); }), dec_bytes);
+    report("b2b: enc CH1", 8, time_us([&] { enc_kernel<1, false, true, false><<<g8, 256>>>(s); }), enc_bytes);
+    report("b2b: dec", 2, time_us([&] { dec_kernel<true, true><<<g2, 256>>>(d); }), dec_bytes);
+  }
+  CHECK(hipFree(objs));
+  CHECK(hipFree(out));
+  CHECK(hipFree(frags_raw));
+  CHECK(hipFree(sink));
   return 0;
 }
