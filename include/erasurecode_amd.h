@@ -228,6 +228,16 @@ int ecamd_reconstruct_host_batch(int desc, const void *h_frags, uint64_t frag_st
 /* Device ordinal used by this process (hipGetDevice at create time). */
 int ecamd_device(int desc);
 
+/* The decode matrix the kernels apply for one erasure pattern (needs no GPU;
+ * liberasurecode_rs_vand's decode: rows of inverse(G[avail]), the first k
+ * available fragments avail[0..k-1] ascending).  dest = -1: one row per
+ * missing data fragment; dest >= 0: the row rebuilding fragment dest.
+ * rows: up to k rows x k u16 coefficients (GF(2^16); GF(2^8) values for the
+ * ISA-L codes); out_idx: the fragment index each row produces.  Returns the
+ * row count, or -EINVALIDPARAMS / -EINSUFFFRAGS (singular submatrix). */
+int ecamd_decode_matrix(int backend_id, int k, int m, const int *avail, int dest, uint16_t *rows,
+                        int *out_idx);
+
 /* Does a batch layout fit the kernels' 32-bit buffer offsets?  0, or
  * -EINVALIDPARAMS when it does not: k*blocksize + 16 (an object's slices;
  * decode's output window holds 2^31 - 1 bytes), (k+m)*frag_stride (a stripe's

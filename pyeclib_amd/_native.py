@@ -140,6 +140,9 @@ _sig = {
     "liberasurecode_get_version": (ctypes.c_uint32, []),
     "ecamd_blocksize": (ctypes.c_uint64, [ctypes.c_int, ctypes.c_uint64]),
     "ecamd_device": (ctypes.c_int, [ctypes.c_int]),
+    "ecamd_decode_matrix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           _P(ctypes.c_int), ctypes.c_int,
+                                           _P(ctypes.c_uint16), _P(ctypes.c_int)]),
     "ecamd_layout_supported": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                               ctypes.c_uint64, ctypes.c_uint64,
                                               ctypes.c_uint64]),

@@ -28,6 +28,7 @@ __device__ __forceinline__ uint32_t zmap(uint32_t r, uint32_t tab) {
 #pragma unroll
   for (int b = 0; b < 4; ++b)
     a ^= lds32(tab + 128 * b + byte_of(lo, b)) ^ lds32(tab + 128 * b + 64 + byte_of(hi, b));
+  asm volatile("" : "+v"(a));  // materialised here (see raw16)
   return a;
 }
 
@@ -45,8 +46,12 @@ __device__ __forceinline__ uint32_t raw16(const uint4& x, uint32_t tab) {
       a ^= lds32(tab + 64 * p + byte_of(lo, b)) ^ lds32(tab + 64 * (p + 1) + byte_of(hi, b));
     }
     // one dword's 8 lookups at a time: otherwise hipcc hoists all 32 (and
-    // those of the next call) ahead of the XORs, one VGPR each
+    // those of the next call) ahead of the XORs, one VGPR each.  The pin
+    // keeps the XORs from sinking, the memory clobber the lookups from
+    // rising, at the IR level (ec_kernels_impl.hpp lookup_fence).
+    asm volatile("" : "+v"(a));
     __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" ::: "memory");
   }
   return a;
 }

@@ -61,6 +61,8 @@ struct EncodeParams {
   uint32_t bs;              // payload bytes per fragment
   uint32_t n_obj;
   uint32_t tiles, edge_tiles;  // set by the launcher: interior / edge items per object
+  uint32_t tile_ch;            // set by the launcher: an interior item spans tile_ch * 4 KiB
+                               // (edge items 4 KiB each, from tiles * tile_ch * 4 KiB on)
   uint32_t xcd_split;          // set by the launcher (item_range)
   uint32_t fused_edges;        // set by the launcher: edge items run in the interior launch
   // inline_crc32 fused into the encode (null: no parity CRC in this launch):

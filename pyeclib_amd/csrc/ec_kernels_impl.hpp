@@ -144,6 +144,20 @@ __device__ __forceinline__ void buf_st(Rsrc r, uint32_t voff, uint32_t soff, con
   st_fence();
 }
 
+// Between the lookup groups of one input: keeps hipcc from hoisting every
+// LDS lookup of the unrolled input loop ahead of the XORs that consume them
+// (2 VGPRs each).  The scheduling barrier alone holds only in the machine
+// scheduler: for small k (2..6) the IR passes had moved all 128 lookups of an
+// item to its top and sunk the XORs to the stores (256 VGPRs unconstrained,
+// up to 1.4 KB per lane of spills at the 64-VGPR budget).  The empty asm with
+// a memory clobber keeps the lookups in place at the IR level, and each
+// accumulator group is pinned (empty asm on it) right after its XORs so they
+// cannot sink; neither emits an instruction.
+__device__ __forceinline__ void lookup_fence() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+
 // a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -234,11 +248,13 @@ struct Gf16 {
       s_lo.y = xor3(xor3(s_lo.y, e0.y, e1.y), e2.y, e3.y);
       s_hi.x = xor3(xor3(s_hi.x, e4.x, e5.x), e6.x, e7.x);
       s_hi.y = xor3(xor3(s_hi.y, e4.y, e5.y), e6.y, e7.y);
+      asm volatile("" : "+v"(s_lo.x), "+v"(s_lo.y), "+v"(s_hi.x), "+v"(s_hi.y));
     } else {
       s_lo.x = xor3(xor3(s_lo.x, lds_u32(a[0], tab + qoff(0)), lds_u32(a[1], tab + qoff(1))),
                     lds_u32(a[2], tab + qoff(2)), lds_u32(a[3], tab + qoff(3)));
       s_hi.x = xor3(xor3(s_hi.x, lds_u32(a[4], tab + qoff(0)), lds_u32(a[5], tab + qoff(1))),
                     lds_u32(a[6], tab + qoff(2)), lds_u32(a[7], tab + qoff(3)));
+      asm volatile("" : "+v"(s_lo.x), "+v"(s_hi.x));
     }
   }
   // One symbol (h = 0: low half-word) of x at a time: half the lookup
@@ -256,11 +272,13 @@ struct Gf16 {
                     e2 = lds_u64(a[4 * h + 2], tab + qoff(2)), e3 = lds_u64(a[4 * h + 3], tab + qoff(3));
         s.x = xor3(xor3(s.x, e0.x, e1.x), e2.x, e3.x);
         s.y = xor3(xor3(s.y, e0.y, e1.y), e2.y, e3.y);
+        asm volatile("" : "+v"(s.x), "+v"(s.y));
       } else {
         s.x = xor3(xor3(s.x, lds_u32(a[4 * h], tab + qoff(0)), lds_u32(a[4 * h + 1], tab + qoff(1))),
                    lds_u32(a[4 * h + 2], tab + qoff(2)), lds_u32(a[4 * h + 3], tab + qoff(3)));
+        asm volatile("" : "+v"(s.x));
       }
-      __builtin_amdgcn_sched_barrier(0);
+      lookup_fence();
     }
   }
   // The scheduling barriers stop hipcc from hoisting every LDS lookup of the
@@ -275,13 +293,13 @@ struct Gf16 {
       return;
     }
     mac_dword<Z>(kb, tab, x.x, a.s[0], a.s[1]);
-    __builtin_amdgcn_sched_barrier(0);
+    lookup_fence();
     mac_dword<Z>(kb, tab, x.y, a.s[2], a.s[3]);
-    __builtin_amdgcn_sched_barrier(0);
+    lookup_fence();
     mac_dword<Z>(kb, tab, x.z, a.s[4], a.s[5]);
-    __builtin_amdgcn_sched_barrier(0);
+    lookup_fence();
     mac_dword<Z>(kb, tab, x.w, a.s[6], a.s[7]);
-    __builtin_amdgcn_sched_barrier(0);
+    lookup_fence();
   }
   static __device__ __forceinline__ uint32_t pack(const uint2& lo, const uint2& hi, int r) {
     const uint32_t a = (r < 2) ? lo.x : lo.y;
@@ -323,17 +341,18 @@ struct Gf8 {
       a[b] = xor3(a[b], lds_u32(__builtin_amdgcn_perm(kb, ylo, sel), tab),
                   lds_u32(__builtin_amdgcn_perm(kb, yhi, sel), tab));
     }
+    asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]));
   }
   template <bool Z = false, bool SPLIT = false>
   static __device__ __forceinline__ void mac(uint32_t kb, uint32_t tab, const uint4& x, Acc& a) {
     mac_dword(kb, tab, x.x, a.a + 0);
-    __builtin_amdgcn_sched_barrier(0);
+    lookup_fence();
     mac_dword(kb, tab, x.y, a.a + 4);
-    __builtin_amdgcn_sched_barrier(0);
+    lookup_fence();
     mac_dword(kb, tab, x.z, a.a + 8);
-    __builtin_amdgcn_sched_barrier(0);
+    lookup_fence();
     mac_dword(kb, tab, x.w, a.a + 12);
-    __builtin_amdgcn_sched_barrier(0);
+    lookup_fence();
   }
   // 4x4 byte transpose: byte b of the result is byte r of a[b].
   static __device__ __forceinline__ uint32_t pack(const uint32_t* a, int r) {
@@ -412,6 +431,19 @@ __device__ __forceinline__ void store_partial(uint8_t* dst, const uint4& v, int6
     return;
   }
   put_bytes(dst, v, 0, static_cast<uint32_t>(n));
+}
+
+// The first n (> 0) bytes of v, the rest of the 16-B unit zeroed: a
+// fragment payload's last unit, whose bytes past the payload are slot
+// padding (frag_stride >= 80 + round16(bs)), is then stored whole.
+__device__ __forceinline__ uint4 zero_tail(const uint4& v, int64_t n) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int64_t valid = n - 4 * i;
+    w[i] &= valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : (1u << (8 * valid)) - 1u);
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // Whole block copies `bytes` of tables from global memory to LDS byte `dst`.
@@ -528,6 +560,12 @@ __host__ __device__ constexpr int stream_slots() {
 // encode keeps 8 (302.1 us vs 302.9 at 6, 304.4 at 7).
 constexpr int kEncodeOcc = 8, kEncodePerCu = 8;
 constexpr int kEncodeCrcOcc = 5;  // the fused-CRC encode's register budget (96 VGPRs)
+// Full-stripe encode (data fragments stored too): no register cap.  Capped
+// at 64 VGPRs the edge items' extra stores spilled (44 B per lane of
+// scratch), and hipcc still spilled 12 B at a 72 cap; uncapped it takes 70
+// (k = 10: 7 waves per SIMD), and the launcher sizes the grid from the
+// kernel's actual register count (resident_per_cu).
+constexpr int kEncodeDataOcc = 1;
 constexpr int kDecodeOcc = 4, kDecodePerCu = 2;
 // Reconstruct (k reads, one row written) keeps 4 per CU: at 2 the config-3
 // reconstruct (GF(2^8), k = 12, 16 MiB) ran 0.586 ms vs 0.500 before.
@@ -543,10 +581,12 @@ constexpr bool kDecodeXcd = false;
 // Interior item w: 4 KiB of payload positions starting at t0 = tile*4096;
 // this wave's chunk at t0 + 1024*wave, the lane at + 16*lane (voffset).
 constexpr uint32_t kTile = kWavesPerBlock * kChunkBytes;
+// CH chunks per wave: the item spans CH * 4 KiB, the wave CH KiB of it.
+template <int CH = 1>
 __device__ __forceinline__ void enc_item_pos(const EncodeParams& p, uint32_t w, uint32_t& o,
                                              uint32_t& x) {
   o = w / p.tiles;
-  x = (w - o * p.tiles) * kTile + wave_in_block() * kChunkBytes;
+  x = (w - o * p.tiles) * (kTile * CH) + wave_in_block() * (kChunkBytes * CH);
 }
 
 // Inputs an edge item holds in registers at once (edge items run inside the
@@ -559,7 +599,7 @@ constexpr int kEdgeGroup = 1;
 template <class F, int K, int NR, bool DATA>
 __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t e) {
   const uint32_t o = e / p.edge_tiles;
-  const uint32_t t = (p.tiles + (e - o * p.edge_tiles)) * kTile + threadIdx.x * 16;
+  const uint32_t t = (p.tiles * p.tile_ch + (e - o * p.edge_tiles)) * kTile + threadIdx.x * 16;
   if (t >= p.bs) return;
   const uint8_t* obj = p.objs + static_cast<uint64_t>(o) * p.obj_stride;
   const int64_t rem = static_cast<int64_t>(p.bs) - t;
@@ -568,6 +608,8 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
   // register budget it must not raise
   typename F::Acc s;
   F::zero(s);
+  Rsrc dat;
+  if constexpr (DATA) dat = rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride);
 #pragma unroll
   for (int j0 = 0; j0 < K; j0 += kEdgeGroup) {
     constexpr int G = kEdgeGroup;
@@ -579,20 +621,24 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
     for (int j = 0; j < G; ++j)
       if (j0 + j < K) F::template mac<true>(F::kb(0), (j0 + j) * F::kTableBytes, x[j], s);
     if constexpr (DATA) {
+      // one 16-B store per input through the object's data descriptor (an
+      // address pair per input, or the byte loop of store_partial, made
+      // hipcc spill the streaming kernel)
 #pragma unroll
       for (int j = 0; j < G; ++j)
         if (j0 + j < K)
-          store_partial(p.data + static_cast<uint64_t>(o) * p.stripe_stride +
-                            static_cast<uint64_t>(j0 + j) * p.frag_stride + kHeaderBytes + t,
-                        x[j], rem);
+          buf_st(dat, t, (j0 + j) * p.frag_stride + kHeaderBytes, zero_tail(x[j], rem));
     }
     __builtin_amdgcn_sched_barrier(0);
   }
   F::pin(s);
-  uint8_t* par = p.parity + static_cast<uint64_t>(o) * p.stripe_stride + p.row0 * p.frag_stride +
-                 kHeaderBytes + t;
+  // the payload's last unit is stored whole with its bytes past bs zeroed
+  // (slot padding): no byte loop (store_partial's, inlined here, put up to
+  // 1.4 KB per lane of scratch in the small-k kernels)
+  const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
 #pragma unroll
-  for (int q = 0; q < NR; ++q) store_partial(par + q * p.frag_stride, F::row(s, q), rem);
+  for (int q = 0; q < NR; ++q)
+    buf_st(par, t, (p.row0 + q) * p.frag_stride + kHeaderBytes, zero_tail(F::row(s, q), rem));
 }
 
 // Interior encode: object slices streamed in (default cache policy --
@@ -604,56 +650,72 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
 // -- one pass over the object instead of a separate copy.  NOCOMP:
 // memory-only probe (inputs XORed, no lookups; wrong parity) for the
 // benchmark shape.
-template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false>
+//
+// CH (A/B, k = 10): an item spans CH * 4 KiB of payload positions and each
+// wave takes CH KiB contiguous of every slice; the stream runs chunk-major
+// (the K inputs of chunk 0, its parity stores, then chunk 1 ...), so the
+// registers stay those of CH = 1.  NTL: nontemporal input loads.
+template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false, int CH = 1,
+          bool NTL = false, int NBX = 0>
 __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
-  constexpr int NB = stream_bufs<K>();
+  constexpr int NB = NBX ? NBX : stream_bufs<K>();  // NBX: A/B (divides K)
   const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
   uint32_t w = r.begin;
   if (w >= r.end) return;
   uint32_t o, x;
-  enc_item_pos(p, w, o, x);
+  enc_item_pos<CH>(p, w, o, x);
   Rsrc cur = rsrc(p.objs + static_cast<uint64_t>(o) * p.obj_stride);
   const uint32_t lane16 = lane_id() * 16;
   constexpr int KP = stream_slots<K, NB>();
+  constexpr int SL = KP * CH;  // stream slots per item: slot i = chunk i / KP, input i % KP
   uint4 buf[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j)
-    if (j < K) buf[j] = buf_ld<true>(cur, lane16, j * p.bs + x);
+    if (j < K) buf[j] = buf_ld<!NTL>(cur, lane16, j * p.bs + x);
+  // one item per trip: hipcc would otherwise unroll the item loop for small k
+  // (k = 2..6: 256 VGPRs unconstrained, up to 1.4 KB per lane of spills at 64)
+#pragma clang loop unroll(disable)
   while (true) {
     // the next item, or this one again through a zero-record descriptor
     const uint32_t wn = w + r.step < r.end ? w + r.step : w;
     uint32_t on, xn;
-    enc_item_pos(p, wn, on, xn);
+    enc_item_pos<CH>(p, wn, on, xn);
     const Rsrc nxt = rsrc(p.objs + static_cast<uint64_t>(on) * p.obj_stride, wn == w ? 0 : -1);
     Rsrc dat;
     if constexpr (DATA) dat = rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride);
+    const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
     typename F::Acc s;
     F::zero(s);
 #pragma unroll
-    for (int j = 0; j < KP; ++j) {
+    for (int i = 0; i < SL; ++i) {
+      const int j = i % KP, c = i / KP;
       if (j < K) {
         if constexpr (NOCOMP) {
           uint32_t* a = reinterpret_cast<uint32_t*>(&s);
-          a[0] ^= buf[j % NB].x;
-          a[2] ^= buf[j % NB].y;
-          a[4] ^= buf[j % NB].z;
-          a[6] ^= buf[j % NB].w;
+          a[0] ^= buf[i % NB].x;
+          a[2] ^= buf[i % NB].y;
+          a[4] ^= buf[i % NB].z;
+          a[6] ^= buf[i % NB].w;
         } else {
-          F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[j % NB], s);
+          F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[i % NB], s);
         }
-        if constexpr (DATA) buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x, buf[j % NB]);
+        if constexpr (DATA)
+          buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x + kChunkBytes * c, buf[i % NB]);
       }
-      if (j + NB < KP) {
-        if (j + NB < K) buf[j % NB] = buf_ld<true>(cur, lane16, (j + NB) * p.bs + x);
-      } else if (j + NB - KP < K) {
-        buf[j % NB] = buf_ld<true>(nxt, lane16, (j + NB - KP) * p.bs + xn);
+      const int in = i + NB;  // slot refilled into this buffer
+      if (in < SL) {
+        if (in % KP < K) buf[i % NB] = buf_ld<!NTL>(cur, lane16, (in % KP) * p.bs + x + kChunkBytes * (in / KP));
+      } else if ((in - SL) % KP < K) {
+        buf[i % NB] = buf_ld<!NTL>(nxt, lane16, ((in - SL) % KP) * p.bs + xn + kChunkBytes * ((in - SL) / KP));
+      }
+      if (j == KP - 1) {  // chunk c complete: its parity rows
+        F::pin(s);
+        const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x + kChunkBytes * c;
+#pragma unroll
+        for (int q = 0; q < NR; ++q) buf_st(par, lane16, soff + q * p.frag_stride, F::row(s, q));
+        if (c + 1 < CH) F::zero(s);
       }
     }
-    F::pin(s);
-    const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
-    const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x;
-#pragma unroll
-    for (int q = 0; q < NR; ++q) buf_st(par, lane16, soff + q * p.frag_stride, F::row(s, q));
     if (wn == w) break;
     w = wn;
     o = on;
@@ -683,13 +745,15 @@ __device__ __forceinline__ void encode_edges(const EncodeParams& p, uint32_t fir
 // profiles/r02l_timeline.txt): with the edges in a launch of their own on a
 // side stream, the fork / join left the GPU idle 25-32 us between
 // consecutive interior kernels.
-template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false>
+template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false, int CH = 1,
+          bool NTL = false, int NBX = 0>
 __global__ void __launch_bounds__(kThreadsPerBlock)
-    __attribute__((amdgpu_waves_per_eu(kEncodeOcc, 8))) encode_kernel(EncodeParams p) {
+    __attribute__((amdgpu_waves_per_eu(DATA ? kEncodeDataOcc : (NBX > 6 ? 4 : kEncodeOcc), 8)))
+    encode_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
   __syncthreads();
   if (p.fused_edges) encode_edges<F, K, NR, DATA>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
-  encode_interior<F, K, NR, NOCOMP, DATA>(p);
+  encode_interior<F, K, NR, NOCOMP, DATA, CH, NTL, NBX>(p);
 }
 
 // Headers and edge items of an encode in a launch of their own (the
@@ -793,6 +857,9 @@ __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
   uint32_t acc[NR];
 #pragma unroll
   for (int q = 0; q < NR; ++q) acc[q] = 0;
+  // one item per trip: hipcc would otherwise unroll the item loop for small k
+  // (k = 2..6: 256 VGPRs unconstrained, up to 1.4 KB per lane of spills at 64)
+#pragma clang loop unroll(disable)
   while (true) {
     const uint32_t wn = w + 1 < end ? w + 1 : w;
     uint32_t on, xn;
@@ -1039,6 +1106,9 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
   for (int j = 0; j < NB; ++j)
     if (j < K) buf[j] = buf_ld(cur, lane16, in_pos(p, d, j) * p.frag_stride + kHeaderBytes + x);
   table_prefetch<F, K>(p, d.table(), d.n_out() != 0, pre);
+  // one item per trip: hipcc would otherwise unroll the item loop for small k
+  // (k = 2..6: 256 VGPRs unconstrained, up to 1.4 KB per lane of spills at 64)
+#pragma clang loop unroll(disable)
   while (true) {
     const uint32_t wn = w + r.step < r.end ? w + r.step : w;
     uint32_t on, xn;
@@ -1313,10 +1383,17 @@ inline int64_t last_room(uint32_t bs, uint64_t obj_len, uint32_t k) {
 // the data fragments.  Interior tiles: 4 KiB of positions ending at or before
 // min(bs, room).  ECAMD_ENC_NOCOMP=1: memory-only probe of the benchmark
 // shape (tools/ab_bench.py).
+// Interior items of `ch` * 4 KiB: the tiles and the 4-KiB edge tiles past them.
+inline void set_tiles(EncodeParams& p, int64_t room, uint32_t ch) {
+  p.tile_ch = ch;
+  p.tiles = static_cast<uint32_t>(room / (kTile * ch));
+  p.edge_tiles = (p.bs + kTile - 1) / kTile - p.tiles * ch;
+}
+
 template <class F, int K, int NR>
 hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
-  p.tiles = static_cast<uint32_t>(last_room(p.bs, p.obj_len, K) / kTile);
-  p.edge_tiles = (p.bs + kTile - 1) / kTile - p.tiles;
+  const int64_t room = last_room(p.bs, p.obj_len, K);
+  set_tiles(p, room, 1);
   constexpr size_t lds = K * F::kTableBytes;
   // data fragments are written by the first pass (rows 0..3) only
   const bool data = p.data != nullptr && p.row0 == 0;
@@ -1325,6 +1402,25 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   if constexpr (K == 10 && NR == 4) {
     probe = env_flag("ECAMD_ENC_NOCOMP", false);
     per_cu = env_int("ECAMD_ENC_PER_CU", kEncodePerCu);  // A/B
+    // A/B: CH KiB per wave and slice (ECAMD_ENC_CH=2), nontemporal loads
+    // (ECAMD_ENC_NTL=1); plain encode (no CRC, no data fragments) only
+    const int ch = env_int("ECAMD_ENC_CH", 1);
+    const bool ntl = env_flag("ECAMD_ENC_NTL", false);
+    const int nb = env_int("ECAMD_ENC_NB", 0);  // 10: every input of an item in flight
+    if (p.crc_tables == nullptr && !data && !probe && (ch == 2 || ntl || nb == 10) &&
+        !env_flag("ECAMD_EDGE_SIDE", false)) {
+      p.fused_edges = 1;
+      if (ch == 2) set_tiles(p, room, 2);
+      const uint32_t items = std::max({p.n_obj * p.tiles, p.n_obj * p.edge_tiles,
+                                       p.headers ? p.n_obj : 0u});
+      if (nb == 10)
+        return ntl ? launch(encode_kernel<F, K, NR, false, false, 1, true, 10>, p, lds, items, stream, per_cu)
+                   : launch(encode_kernel<F, K, NR, false, false, 1, false, 10>, p, lds, items, stream, per_cu);
+      if (ch == 2)
+        return ntl ? launch(encode_kernel<F, K, NR, false, false, 2, true>, p, lds, items, stream, per_cu)
+                   : launch(encode_kernel<F, K, NR, false, false, 2, false>, p, lds, items, stream, per_cu);
+      return launch(encode_kernel<F, K, NR, false, false, 1, true>, p, lds, items, stream, per_cu);
+    }
   }
   hipError_t e;
   if (p.crc_tables != nullptr) {

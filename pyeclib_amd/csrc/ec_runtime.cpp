@@ -560,37 +560,90 @@ void build_tables(int w, const uint16_t* rows, int nrows, int k, uint8_t* out) {
 
 // Rows of a decode (dest < 0) or reconstruct (dest >= 0) matrix over the
 // inputs `avail` (first k available fragment indices, ascending).
-bool pattern_rows(const Instance& I, const int* avail, int dest, std::vector<uint16_t>& rows,
-                  std::vector<int>& out_idx) {
-  const int k = I.k, w = I.code.w;
-  GfMatrix sub(static_cast<size_t>(k) * k), inv;
-  for (int i = 0; i < k; ++i)
-    std::memcpy(&sub[i * k], &I.gen[avail[i] * k], sizeof(uint16_t) * k);
-  if (!gf_invert(w, sub, inv, k)) return false;
+//
+// The rows are those of inverse(G[avail]) (liberasurecode_rs_vand's decode
+// matrix), found without the k x k inversion: G's top is the identity, so
+// with D the e missing data indices and P the e parity inputs, the parity
+// equations read  par_P = A d_D + B d_present  (A = G[P][D], e x e;
+// B = G[P][present]), hence  d_D = inv(A) par_P + inv(A) B d_present  (char 2).
+// One e x e inversion (e <= m) and an e x e x (k - e) product replace a
+// k x k Gauss-Jordan: measured round 3, per-call decode with erasures that
+// change every call spent most of its host time here.  The inverse is unique,
+// so the rows -- and every byte decoded -- are the same.
+bool decode_rows(int k, int w, const GfMatrix& gen, const int* avail, int dest,
+                 std::vector<uint16_t>& rows, std::vector<int>& out_idx) {
+  int pos_of[kMaxFragments];  // input position of data index j, or -1
+  for (int j = 0; j < k; ++j) pos_of[j] = -1;
+  int par_pos[kMaxFragments], n_par = 0;
+  for (int c = 0; c < k; ++c) {
+    if (avail[c] < k)
+      pos_of[avail[c]] = c;
+    else
+      par_pos[n_par++] = c;
+  }
+  int miss[kMaxFragments], e = 0;
+  for (int j = 0; j < k; ++j)
+    if (pos_of[j] < 0) miss[e++] = j;
+  if (e != n_par) return false;  // k inputs: every missing data index has a parity input
+  // R[t]: row of missing data index miss[t] over the k inputs
+  std::vector<uint16_t> R(static_cast<size_t>(e) * k, 0);
+  if (e > 0) {
+    GfMatrix A(static_cast<size_t>(e) * e), Ainv;
+    for (int r = 0; r < e; ++r)
+      for (int t = 0; t < e; ++t) A[r * e + t] = gen[avail[par_pos[r]] * k + miss[t]];
+    if (!gf_invert(w, A, Ainv, e)) return false;
+    for (int t = 0; t < e; ++t) {
+      uint16_t* row = &R[static_cast<size_t>(t) * k];
+      for (int r = 0; r < e; ++r) row[par_pos[r]] = Ainv[t * e + r];
+      for (int j = 0; j < k; ++j) {
+        const int c = pos_of[j];
+        if (c < 0) continue;
+        uint16_t acc = 0;
+        for (int r = 0; r < e; ++r)
+          acc ^= gf_mul(w, Ainv[t * e + r], gen[avail[par_pos[r]] * k + j]);
+        row[c] = acc;
+      }
+    }
+  }
+  int miss_t[kMaxFragments];  // index into R of missing data index j
+  for (int t = 0; t < e; ++t) miss_t[miss[t]] = t;
   rows.clear();
   out_idx.clear();
   if (dest < 0) {
-    std::vector<bool> present(k, false);
-    for (int i = 0; i < k; ++i)
-      if (avail[i] < k) present[avail[i]] = true;
-    for (int j = 0; j < k; ++j)
-      if (!present[j]) {
-        rows.insert(rows.end(), inv.begin() + j * k, inv.begin() + (j + 1) * k);
-        out_idx.push_back(j);
-      }
+    for (int t = 0; t < e; ++t) {
+      rows.insert(rows.end(), R.begin() + static_cast<size_t>(t) * k,
+                  R.begin() + static_cast<size_t>(t + 1) * k);
+      out_idx.push_back(miss[t]);
+    }
   } else if (dest < k) {
-    rows.assign(inv.begin() + dest * k, inv.begin() + (dest + 1) * k);
+    rows.assign(k, 0);
+    if (pos_of[dest] >= 0)
+      rows[pos_of[dest]] = 1;
+    else
+      rows.assign(R.begin() + static_cast<size_t>(miss_t[dest]) * k,
+                  R.begin() + static_cast<size_t>(miss_t[dest] + 1) * k);
     out_idx.push_back(dest);
   } else {
+    // parity row dest over the inputs: sum over data j of G[dest][j] * (row of d_j)
     rows.assign(k, 0);
-    for (int c = 0; c < k; ++c) {
-      uint16_t acc = 0;
-      for (int j = 0; j < k; ++j) acc ^= gf_mul(w, I.gen[dest * k + j], inv[j * k + c]);
-      rows[c] = acc;
+    for (int j = 0; j < k; ++j) {
+      const uint16_t g = gen[dest * k + j];
+      if (g == 0) continue;
+      if (pos_of[j] >= 0) {
+        rows[pos_of[j]] ^= g;
+      } else {
+        const uint16_t* row = &R[static_cast<size_t>(miss_t[j]) * k];
+        for (int c = 0; c < k; ++c) rows[c] ^= gf_mul(w, g, row[c]);
+      }
     }
     out_idx.push_back(dest);
   }
   return true;
+}
+
+bool pattern_rows(const Instance& I, const int* avail, int dest, std::vector<uint16_t>& rows,
+                  std::vector<int>& out_idx) {
+  return decode_rows(I.k, I.code.w, I.gen, avail, dest, rows, out_idx);
 }
 
 // Table slot for (avail set, dest): `passes` consecutive table sets in the pool.
@@ -1638,6 +1691,26 @@ int ecamd_layout_supported(int k, int m, int w, uint64_t obj_len, uint64_t frag_
                            uint64_t n_obj) {
   if (k < 1 || m < 1 || k + m > kMaxFragments || (w != 8 && w != 16)) return -EINVALIDPARAMS;
   return layout_fits(k, m, blocksize_of(k, w, obj_len), frag_stride, n_obj) ? 0 : -EINVALIDPARAMS;
+}
+
+int ecamd_decode_matrix(int backend_id, int k, int m, const int* avail, int dest, uint16_t* rows,
+                        int* out_idx) {
+  const Code* code = code_of(backend_id);
+  if (!code || !avail || !rows || !out_idx || k < 1 || m < 1 || k + m > kMaxFragments ||
+      dest < -1 || dest >= k + m)
+    return -EINVALIDPARAMS;
+  for (int c = 0; c < k; ++c)
+    if (avail[c] < 0 || avail[c] >= k + m || (c > 0 && avail[c] <= avail[c - 1]))
+      return -EINVALIDPARAMS;
+  const GfMatrix gen = code->w == 16 ? make_generator(k, m)
+                       : backend_id == EC_BACKEND_ISA_L_RS_CAUCHY ? make_isal_cauchy_matrix(k, m)
+                                                                  : make_isal_rs_matrix(k, m);
+  std::vector<uint16_t> r;
+  std::vector<int> o;
+  if (!decode_rows(k, code->w, gen, avail, dest, r, o)) return -EINSUFFFRAGS;
+  std::memcpy(rows, r.data(), r.size() * sizeof(uint16_t));
+  std::memcpy(out_idx, o.data(), o.size() * sizeof(int));
+  return static_cast<int>(o.size());
 }
 
 int ecamd_device(int desc) {
