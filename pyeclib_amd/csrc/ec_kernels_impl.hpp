@@ -103,11 +103,12 @@ constexpr int kNt = 2;
 // range check drops them), which is how a wave's last item "prefetches"
 // nothing while keeping the instruction stream -- and so hipcc's wait
 // counts -- identical to every other item.
+__device__ __forceinline__ uint32_t to_sgpr(uint32_t v);
 __device__ __forceinline__ Rsrc rsrc(const void* base, int records = -1) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
   const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
-  const int n = static_cast<int>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(records)));
+  const int n = static_cast<int>(to_sgpr(static_cast<uint32_t>(records)));
   return __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, n, 0x00020000);
 }
@@ -377,6 +378,18 @@ __device__ __forceinline__ uint32_t wave_in_block() {
   return __builtin_amdgcn_readfirstlane(threadIdx.x / kLanes);
 }
 
+// A wave-uniform value computed by VALU code (a 32-bit division by a runtime
+// divisor has no scalar form) moved into an SGPR.  hipcc drops a plain
+// readfirstlane of a value it already knows to be uniform, then keeps the
+// value in a VGPR, and every buffer access whose descriptor or soffset
+// derives from it is wrapped in a waterfall loop (round 3: 10 per item in the
+// decode stream, found in the generated code).  The empty asm hides the
+// uniformity, so the readfirstlane stays.
+__device__ __forceinline__ uint32_t to_sgpr(uint32_t v) {
+  asm("" : "+v"(v));
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
 // 16 bytes at base+off; bytes at or past `len` read as zero (encode padding).
 // Two 16-B loads at 16-B-aligned offsets inside [0, round16(len)) -- the
 // object's buffer spans at least that (obj_stride is a multiple of 16 and
@@ -559,7 +572,12 @@ __host__ __device__ constexpr int stream_slots() {
 // r02r_ab_per_cu.txt: 405.8 us at 2, 411.8 at 3, 424.1 at 4, 424.5 at 5);
 // encode keeps 8 (302.1 us vs 302.9 at 6, 304.4 at 7).
 constexpr int kEncodeOcc = 8, kEncodePerCu = 8;
-constexpr int kEncodeCrcOcc = 5;  // the fused-CRC encode's register budget (96 VGPRs)
+// The fused-CRC encode's register budget: 7 waves per SIMD (72 VGPRs, no
+// scratch at k = 10, m = 4) once its item range stopped feeding waterfall
+// loops (encode_crc_interior); 6 with six inputs in flight (k = 18, 24,
+// 30: 72 VGPRs spilled 8-36 B); the full-stripe form (data fragments stored
+// too) keeps 5.
+constexpr int kEncodeCrcOcc = 7, kEncodeCrcDataOcc = 5;
 // Full-stripe encode (data fragments stored too): no register cap.  Capped
 // at 64 VGPRs the edge items' extra stores spilled (44 B per lane of
 // scratch), and hipcc still spilled 12 B at a 72 cap; uncapped it takes 70
@@ -585,7 +603,7 @@ constexpr uint32_t kTile = kWavesPerBlock * kChunkBytes;
 template <int CH = 1>
 __device__ __forceinline__ void enc_item_pos(const EncodeParams& p, uint32_t w, uint32_t& o,
                                              uint32_t& x) {
-  o = w / p.tiles;
+  o = to_sgpr(w / p.tiles);
   x = (w - o * p.tiles) * (kTile * CH) + wave_in_block() * (kChunkBytes * CH);
 }
 
@@ -745,10 +763,21 @@ __device__ __forceinline__ void encode_edges(const EncodeParams& p, uint32_t fir
 // profiles/r02l_timeline.txt): with the edges in a launch of their own on a
 // side stream, the fork / join left the GPU idle 25-32 us between
 // consecutive interior kernels.
+// Register budget (waves per SIMD) of an encode instantiation.  GF(2^8)
+// with k >= 18 (six inputs in flight, 4-byte table entries) spilled 12 B per
+// lane at 64 VGPRs and gets 72.
+template <class F, int K, bool DATA, int NBX>
+__host__ __device__ constexpr int encode_occ() {
+  if (DATA) return kEncodeDataOcc;
+  if (NBX > 6) return 4;
+  if (F::kW == 8 && K >= 18) return 7;
+  return kEncodeOcc;
+}
+
 template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false, int CH = 1,
           bool NTL = false, int NBX = 0>
 __global__ void __launch_bounds__(kThreadsPerBlock)
-    __attribute__((amdgpu_waves_per_eu(DATA ? kEncodeDataOcc : (NBX > 6 ? 4 : kEncodeOcc), 8)))
+    __attribute__((amdgpu_waves_per_eu(encode_occ<F, K, DATA, NBX>(), 8)))
     encode_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
   __syncthreads();
@@ -835,13 +864,19 @@ __device__ __forceinline__ uint32_t* crc_part_at(const EncodeParams& p, uint32_t
 
 // Interior with the parity CRC: block b streams the contiguous items
 // [n*b/G, n*(b+1)/G) (ec_crc.hip run_begin), otherwise as encode_interior.
-template <class F, int K, int NR, bool DATA>
+template <class F, int K, int NR, bool DATA, bool NTL = false>
 __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
   constexpr int NB = stream_bufs<K>();
   constexpr uint32_t base = crc_lds_base<F, K>();
   const uint64_t n = static_cast<uint64_t>(p.n_obj) * p.tiles;
-  const uint32_t begin = static_cast<uint32_t>(n * blockIdx.x / gridDim.x);
-  const uint32_t end = static_cast<uint32_t>(n * (blockIdx.x + 1) / gridDim.x);
+  // The 64-bit divisions are expanded into VALU code, so their results sit in
+  // VGPRs; without readfirstlane every buffer access whose soffset derives
+  // from them was wrapped in a waterfall loop (24 of them per item at k = 10,
+  // found round 3 in the generated code).
+  const uint32_t begin =
+      __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n * blockIdx.x / gridDim.x));
+  const uint32_t end =
+      __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n * (blockIdx.x + 1) / gridDim.x));
   uint32_t w = begin;
   if (w >= end) return;
   uint32_t o, x;
@@ -853,7 +888,7 @@ __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
   uint4 buf[NB];
 #pragma unroll
   for (int j = 0; j < NB; ++j)
-    if (j < K) buf[j] = buf_ld<true>(cur, lane16, j * p.bs + x);
+    if (j < K) buf[j] = buf_ld<!NTL>(cur, lane16, j * p.bs + x);
   uint32_t acc[NR];
 #pragma unroll
   for (int q = 0; q < NR; ++q) acc[q] = 0;
@@ -876,9 +911,9 @@ __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
         if constexpr (DATA) buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x, buf[j % NB]);
       }
       if (j + NB < KP) {
-        if (j + NB < K) buf[j % NB] = buf_ld<true>(cur, lane16, (j + NB) * p.bs + x);
+        if (j + NB < K) buf[j % NB] = buf_ld<!NTL>(cur, lane16, (j + NB) * p.bs + x);
       } else if (j + NB - KP < K) {
-        buf[j % NB] = buf_ld<true>(nxt, lane16, (j + NB - KP) * p.bs + xn);
+        buf[j % NB] = buf_ld<!NTL>(nxt, lane16, (j + NB - KP) * p.bs + xn);
       }
     }
     F::pin(s);
@@ -903,16 +938,20 @@ __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
   }
 }
 
-template <class F, int K, int NR, bool DATA = false>
+// NTL: nontemporal input loads (A/B).
+template <class F, int K, int NR, bool DATA = false, bool NTL = false>
 __global__ void __launch_bounds__(kThreadsPerBlock)
-    __attribute__((amdgpu_waves_per_eu(kEncodeCrcOcc, 8))) encode_crc_kernel(EncodeParams p) {
+    __attribute__((amdgpu_waves_per_eu(DATA ? kEncodeCrcDataOcc
+                                            : (stream_bufs<K>() >= 6 ? 6 : kEncodeCrcOcc),
+                                       8)))
+    encode_crc_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
   load_tables(static_cast<const uint32_t*>(p.crc_tables), kCrcLdsBytes, crc_lds_base<F, K>());
   __syncthreads();
   // headers and edge items as encode_kernel; the edge tiles' CRC is taken by
   // crc_finish_kernel from the parity just written
   encode_edges<F, K, NR, DATA>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
-  encode_crc_interior<F, K, NR, DATA>(p);
+  encode_crc_interior<F, K, NR, DATA, NTL>(p);
 }
 
 // Data fragments (optional output of encode): the k padded object slices
@@ -1064,7 +1103,7 @@ __device__ __forceinline__ uint32_t in_pos(const DecodeParams& p, const DescU& d
 
 __device__ __forceinline__ void dec_item_pos(const DecodeParams& p, uint32_t w, uint32_t& o,
                                              uint32_t& x) {
-  o = w / p.tiles;
+  o = to_sgpr(w / p.tiles);
   x = (w - o * p.tiles) * kTile + wave_in_block() * kChunkBytes;
 }
 
@@ -1073,8 +1112,8 @@ __device__ __forceinline__ void dec_item_pos(const DecodeParams& p, uint32_t w, 
 constexpr uint32_t kDrop = 0x80000000u;
 __device__ __forceinline__ Rsrc rsrc_out(const void* base) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
-  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  const uint32_t lo = to_sgpr(static_cast<uint32_t>(a));
+  const uint32_t hi = to_sgpr(static_cast<uint32_t>(a >> 32));
   return __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, 0x7FFFFFFF, 0x00020000);
 }
@@ -1099,12 +1138,14 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
   uint32_t o, x;
   dec_item_pos(p, w, o, x);
   DescU d = load_desc(p, o);
-  Rsrc cur = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride);
   constexpr int KP = stream_slots<K, NB>();
   uint4 buf[NB];
+  {
+    const Rsrc first = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride);
 #pragma unroll
-  for (int j = 0; j < NB; ++j)
-    if (j < K) buf[j] = buf_ld(cur, lane16, in_pos(p, d, j) * p.frag_stride + kHeaderBytes + x);
+    for (int j = 0; j < NB; ++j)
+      if (j < K) buf[j] = buf_ld(first, lane16, in_pos(p, d, j) * p.frag_stride + kHeaderBytes + x);
+  }
   table_prefetch<F, K>(p, d.table(), d.n_out() != 0, pre);
   // one item per trip: hipcc would otherwise unroll the item loop for small k
   // (k = 2..6: 256 VGPRs unconstrained, up to 1.4 KB per lane of spills at 64)
@@ -1114,6 +1155,11 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
     uint32_t on, xn;
     dec_item_pos(p, wn, on, xn);
     const DescU dn = load_desc(p, on);
+    // rebuilt from the object index each trip rather than carried over from
+    // the last trip's `nxt`: the loop-carried 128-bit descriptor was kept in
+    // VGPRs, and every input load went through a waterfall loop (10 per item
+    // at k = 10 until round 3)
+    const Rsrc cur = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride);
     const Rsrc nxt = rsrc(p.frags + static_cast<uint64_t>(on) * p.stripe_stride, wn == w ? 0 : -1);
     const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
     table_prefetch<F, K>(p, dn.table(), wn != w && dn.n_out() != 0 && dn.table() != st.table,
@@ -1159,7 +1205,6 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
     o = on;
     x = xn;
     d = dn;
-    cur = nxt;
   }
 }
 
@@ -1431,10 +1476,18 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
                                      p.headers ? p.n_obj : 0u});
     int grid = 0;
     const int crc_per_cu = env_int("ECAMD_CRC_PER_CU", kEncodePerCu);  // A/B knob
-    e = data ? launch(encode_crc_kernel<F, K, NR, true>, p, crc_lds_bytes<F, K>(), items, stream,
-                      crc_per_cu, false, &grid)
-             : launch(encode_crc_kernel<F, K, NR>, p, crc_lds_bytes<F, K>(), items, stream,
-                      crc_per_cu, false, &grid);
+    bool crc_ntl = false;
+    if constexpr (K == 10 && NR == 4) {
+      crc_ntl = !data && env_flag("ECAMD_CRC_NTL", false);  // A/B
+      if (crc_ntl)
+        e = launch(encode_crc_kernel<F, K, NR, false, true>, p, crc_lds_bytes<F, K>(), items,
+                   stream, crc_per_cu, false, &grid);
+    }
+    if (!crc_ntl)
+      e = data ? launch(encode_crc_kernel<F, K, NR, true>, p, crc_lds_bytes<F, K>(), items, stream,
+                        crc_per_cu, false, &grid)
+               : launch(encode_crc_kernel<F, K, NR>, p, crc_lds_bytes<F, K>(), items, stream,
+                        crc_per_cu, false, &grid);
     if (e != hipSuccess) return e;
     CrcFinishParams fp{};
     fp.parity = p.parity;

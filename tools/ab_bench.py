@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--full-stripe", action="store_true",
                     help="encode writes the k data fragments too (liberasurecode_encode's "
                          "full stripe); checked against the first variant's stripes")
+    ap.add_argument("--alt", action="store_true",
+                    help="alternate encode and decode launches, as bench.py's step does "
+                         "(default: each kernel back to back)")
     args = ap.parse_args()
 
     import torch
@@ -93,25 +96,44 @@ def main():
                 stripes[:, :k].zero_()
             codec.encode(objs, n, parity=stripes[:, k:], data=data)
             codec.decode(stripes, n, masks, out)
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            torch.cuda.synchronize()
-            ev[0].record()
-            for _ in range(args.reps):
-                codec.encode(objs, n, parity=stripes[:, k:], data=data)
-            ev[1].record()
-            for _ in range(args.reps):
-                codec.decode(stripes, n, masks, out)
-            ev[2].record()
-            torch.cuda.synchronize()
-            times[name]["enc"].append(ev[0].elapsed_time(ev[1]) / args.reps * 1e3)
-            times[name]["dec"].append(ev[1].elapsed_time(ev[2]) / args.reps * 1e3)
+            if args.alt:
+                # bench.py's step: encode, decode, encode, ... each kernel
+                # timed by events around it (each pays for the other's
+                # dirty Infinity-Cache lines, as in the bench)
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.reps + 1)]
+                torch.cuda.synchronize()
+                for i in range(args.reps):
+                    ev[2 * i].record()
+                    codec.encode(objs, n, parity=stripes[:, k:], data=data)
+                    ev[2 * i + 1].record()
+                    codec.decode(stripes, n, masks, out)
+                ev[2 * args.reps].record()
+                torch.cuda.synchronize()
+                times[name]["enc"].append(statistics.mean(
+                    ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.reps)) * 1e3)
+                times[name]["dec"].append(statistics.mean(
+                    ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(args.reps)) * 1e3)
+            else:
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                torch.cuda.synchronize()
+                ev[0].record()
+                for _ in range(args.reps):
+                    codec.encode(objs, n, parity=stripes[:, k:], data=data)
+                ev[1].record()
+                for _ in range(args.reps):
+                    codec.decode(stripes, n, masks, out)
+                ev[2].record()
+                torch.cuda.synchronize()
+                times[name]["enc"].append(ev[0].elapsed_time(ev[1]) / args.reps * 1e3)
+                times[name]["dec"].append(ev[1].elapsed_time(ev[2]) / args.reps * 1e3)
             if rnd == 0 and "NOCOMP" not in name:  # NOCOMP probes compute nothing
                 assert torch.equal(stripes, ref_stripes), f"{name}: stripes differ"
                 assert torch.equal(out[:, :n], objs[:, :n]), f"{name}: decode differs"
                 out.zero_()
     apply({})
 
-    print(f"k={k} m={m} {B} x {n} B, {args.rounds} rounds x {args.reps} launches")
+    print(f"k={k} m={m} {B} x {n} B, {args.rounds} rounds x {args.reps} launches, "
+          f"{'alternating encode/decode' if args.alt else 'back to back'}")
     print(f"{'variant':<48} {'enc med us':>10} {'min':>8} {'GB/s':>8} "
           f"{'dec med us':>10} {'min':>8} {'GB/s':>8}")
     for name, _ in variants:

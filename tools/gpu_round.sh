@@ -46,6 +46,9 @@ for s in $STEPS; do
   ab)
     (cd $R && timeout -k 10 400 python3 tools/ab_bench.py ${AB:-base ECAMD_DEC_OCC3=1 ECAMD_XCD=0} > $O/ab.txt 2>&1)
     cat $O/ab.txt ;;
+  abalt)
+    (cd $R && timeout -k 10 400 python3 tools/ab_bench.py --alt ${AB:-base} > $O/ab_alt.txt 2>&1)
+    cat $O/ab_alt.txt ;;
   abfull)
     (cd $R && timeout -k 10 400 python3 tools/ab_bench.py --full-stripe ${ABF:-base ECAMD_DATA_COPY=1} > $O/ab_full.txt 2>&1)
     cat $O/ab_full.txt ;;
@@ -67,6 +70,10 @@ for s in $STEPS; do
     (cd $R && timeout -k 10 300 python3 bench.py --inline-crc32 --steps 10 --no-host \
         --no-cpu-baseline > $O/bench_crc.json 2> $O/bench_crc.err)
     tail -c 400 $O/bench_crc.json ;;
+  crcntl)
+    (cd $R && ECAMD_CRC_NTL=1 timeout -k 10 300 python3 bench.py --inline-crc32 --steps 10 --no-host \
+        --no-cpu-baseline > $O/bench_crc_ntl.json 2> $O/bench_crc_ntl.err)
+    tail -c 400 $O/bench_crc_ntl.json ;;
   bench)
     (cd $R && timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err)
     cat $O/bench.json ;;
