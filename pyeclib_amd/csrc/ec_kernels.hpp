@@ -65,6 +65,8 @@ struct EncodeParams {
                                // (edge items 4 KiB each, from tiles * tile_ch * 4 KiB on)
   uint32_t xcd_split;          // set by the launcher (item_range)
   uint32_t fused_edges;        // set by the launcher: edge items run in the interior launch
+  uint32_t edge_blocks;        // set by the launcher: blocks [0, edge_blocks) run only the edge
+                               // items; 0 = every block runs its share of them first
   // inline_crc32 fused into the encode (null: no parity CRC in this launch):
   // CrcTables (its raw16 / z4096 / level maps), CrcFinishTables for
   // (bs, ceil(bs / 4096)), and n_obj * ceil(bs / 4096) * m u32 of run
@@ -110,6 +112,7 @@ struct DecodeParams {
   uint32_t tiles, edge_tiles;  // set by the launcher: interior / edge items per object
   uint32_t xcd_split;          // set by the launcher (item_range)
   uint32_t fused_edges;        // set by the launcher: edge items run in the interior launch
+  uint32_t edge_blocks;        // set by the launcher (see EncodeParams)
 };
 
 // Dispatch on (p.w, p.k) to the per-k instantiations (ec_dispatch.cpp).

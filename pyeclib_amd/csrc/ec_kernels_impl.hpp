@@ -501,12 +501,20 @@ __device__ __forceinline__ int64_t object_bytes(uint32_t idx, uint32_t bs, uint3
 struct ItemRange {
   uint32_t begin, end, step;
 };
-__device__ __forceinline__ ItemRange item_range(uint32_t items, uint32_t xcd_split) {
-  if (!xcd_split) return {blockIdx.x, items, gridDim.x};
-  const uint32_t x = blockIdx.x & 7u;
+// Interior block b of G: the launch's first edge_blocks blocks (a multiple of
+// 8, so b keeps its XCD) run only edge items (see encode_kernel).
+struct IBlock {
+  uint32_t b, g;
+};
+__device__ __forceinline__ IBlock interior_block(uint32_t edge_blocks) {
+  return {blockIdx.x - edge_blocks, gridDim.x - edge_blocks};
+}
+__device__ __forceinline__ ItemRange item_range(uint32_t items, uint32_t xcd_split, IBlock ib) {
+  if (!xcd_split) return {ib.b, items, ib.g};
+  const uint32_t x = ib.b & 7u;
   const uint32_t lo = static_cast<uint32_t>(static_cast<uint64_t>(items) * x / 8);
   const uint32_t hi = static_cast<uint32_t>(static_cast<uint64_t>(items) * (x + 1) / 8);
-  return {lo + (blockIdx.x >> 3), hi, gridDim.x >> 3};
+  return {lo + (ib.b >> 3), hi, ib.g >> 3};
 }
 
 // Whole block writes `count` 80-byte headers (fragment f at frag0 + f*stride).
@@ -566,12 +574,19 @@ __host__ __device__ constexpr int stream_slots() {
 }
 
 // Waves per SIMD the streaming kernels are built for (register budget) and
-// launched at (blocks per CU; each block has one wave per SIMD).  Decode runs
-// fewer blocks than its budget allows: with the edges fused into the launch,
-// 2 per CU measured best at k = 10 (same process, profiles/r02q_ab_per_cu.txt,
-// r02r_ab_per_cu.txt: 405.8 us at 2, 411.8 at 3, 424.1 at 4, 424.5 at 5);
-// encode keeps 8 (302.1 us vs 302.9 at 6, 304.4 at 7).
-constexpr int kEncodeOcc = 8, kEncodePerCu = 8;
+// launched at (blocks per CU; each block has one wave per SIMD).  Both run
+// fewer blocks than their budget allows: fewer waves streaming at once keep
+// the HBM side more efficient (tools/membench.hip: the encode pattern's best
+// rows are at 1-2 blocks per CU), while 2 still hide the lookups.
+//   decode 2 per CU (same process, profiles/r02q_ab_per_cu.txt,
+//     r02r_ab_per_cu.txt: 405.8 us at 2, 411.8 at 3, 424.1 at 4, 424.5 at 5);
+//   encode 2 per CU once the edge items run in blocks of their own
+//     (launch_edges_apart; round 3, profiles/r03g_ab_alt.txt: 283.2 us at 2
+//     vs 305.8 at 8; at 2 with the edges in front of interior blocks
+//     301.7).  2 is also the best of 2/3/4/8 for k = 2, 4, 6, 7, 8, 12, for
+//     k = 4 m = 2 and for the GF(2^8) codes (profiles/r03h_ab_k*.txt), and
+//     for the fused-CRC encode (339.7 vs 362.6 us at 8).
+constexpr int kEncodeOcc = 8, kEncodePerCu = 2;
 // The fused-CRC encode's register budget: 7 waves per SIMD (72 VGPRs, no
 // scratch at k = 10, m = 4) once its item range stopped feeding waterfall
 // loops (encode_crc_interior); 6 with six inputs in flight (k = 18, 24,
@@ -677,7 +692,7 @@ template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false, int CH
           bool NTL = false, int NBX = 0>
 __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
   constexpr int NB = NBX ? NBX : stream_bufs<K>();  // NBX: A/B (divides K)
-  const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
+  const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split, interior_block(p.edge_blocks));
   uint32_t w = r.begin;
   if (w >= r.end) return;
   uint32_t o, x;
@@ -781,7 +796,14 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
     encode_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
   __syncthreads();
-  if (p.fused_edges) encode_edges<F, K, NR, DATA>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
+  if (p.fused_edges) {
+    if (p.edge_blocks == 0) {
+      encode_edges<F, K, NR, DATA>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
+    } else if (blockIdx.x < p.edge_blocks) {
+      encode_edges<F, K, NR, DATA>(p, blockIdx.x, p.edge_blocks);
+      return;
+    }
+  }
   encode_interior<F, K, NR, NOCOMP, DATA, CH, NTL, NBX>(p);
 }
 
@@ -873,10 +895,9 @@ __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
   // VGPRs; without readfirstlane every buffer access whose soffset derives
   // from them was wrapped in a waterfall loop (24 of them per item at k = 10,
   // found round 3 in the generated code).
-  const uint32_t begin =
-      __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n * blockIdx.x / gridDim.x));
-  const uint32_t end =
-      __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n * (blockIdx.x + 1) / gridDim.x));
+  const IBlock ib = interior_block(p.edge_blocks);
+  const uint32_t begin = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n * ib.b / ib.g));
+  const uint32_t end = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n * (ib.b + 1) / ib.g));
   uint32_t w = begin;
   if (w >= end) return;
   uint32_t o, x;
@@ -950,7 +971,12 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
   __syncthreads();
   // headers and edge items as encode_kernel; the edge tiles' CRC is taken by
   // crc_finish_kernel from the parity just written
-  encode_edges<F, K, NR, DATA>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
+  if (p.edge_blocks == 0) {
+    encode_edges<F, K, NR, DATA>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
+  } else if (blockIdx.x < p.edge_blocks) {
+    encode_edges<F, K, NR, DATA>(p, blockIdx.x, p.edge_blocks);
+    return;
+  }
   encode_crc_interior<F, K, NR, DATA, NTL>(p);
 }
 
@@ -1131,7 +1157,7 @@ template <class F, int K, int MODE, bool NOCOMP = false, int NBX = 0>
 __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st,
                                                 TablePre<F, K>& pre) {
   constexpr int NB = NBX ? NBX : stream_bufs<K>();  // NBX: A/B (divides K)
-  const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split);
+  const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split, interior_block(p.edge_blocks));
   uint32_t w = r.begin;
   if (w >= r.end) return;  // block-uniform: no wave of this block reaches a barrier
   const uint32_t lane16 = lane_id() * 16;
@@ -1287,7 +1313,14 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
     __attribute__((amdgpu_waves_per_eu(NBX > 6 ? 4 : kDecodeOcc, 8))) decode_kernel(DecodeParams p) {
   Slots st{0xFFFFFFFFu, 1u};
   TablePre<F, K> pre;
-  if (p.fused_edges) decode_edges<F, K, MODE>(p, gridDim.x - 1 - blockIdx.x, gridDim.x, st, pre);
+  if (p.fused_edges) {
+    if (p.edge_blocks == 0) {
+      decode_edges<F, K, MODE>(p, gridDim.x - 1 - blockIdx.x, gridDim.x, st, pre);
+    } else if (blockIdx.x < p.edge_blocks) {
+      decode_edges<F, K, MODE>(p, blockIdx.x, p.edge_blocks, st, pre);
+      return;
+    }
+  }
   decode_interior<F, K, MODE, NOCOMP, NBX>(p, st, pre);
 }
 
@@ -1367,6 +1400,44 @@ hipError_t launch(Kern kern, Params p, size_t lds, uint32_t items, hipStream_t s
   return hipGetLastError();
 }
 
+// A launch whose edge items run in blocks of their own: blocks [0, E) take
+// the edge items (E = their count rounded up to 8, at most one per CU) and
+// return; blocks [E, E + G) stream the interior items exactly as a launch of
+// G blocks would.  All E + G blocks must be resident at once -- otherwise
+// interior blocks would queue behind the edge blocks -- else (or with
+// ECAMD_EDGE_BLOCKS=0) every block runs its share of the edge items first.
+// Why: an edge item is a chain of K dependent loads (one input in registers
+// at a time), ~12 us; with the edges at the front of some interior blocks,
+// those blocks finish that much after the rest (measured round 3 at 2 blocks
+// per CU, 256 x 4 MiB k = 10: encode 297.7 us fused, 291.0 with the edges
+// in a launch of their own before it, 284.7 for the interior alone).
+constexpr bool kEdgeBlocks = true;
+template <typename Kern, typename Params>
+hipError_t launch_edges_apart(Kern kern, Params p, size_t lds, uint32_t interior_items,
+                              uint32_t edge_items, hipStream_t stream, int max_per_cu, bool xcd,
+                              int* grid_out = nullptr) {
+  p.edge_blocks = 0;
+  const void* k = reinterpret_cast<const void*>(kern);
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const uint32_t e = (std::min<uint32_t>(edge_items, static_cast<uint32_t>(cus)) + 7u) & ~7u;
+  if (!env_flag("ECAMD_EDGE_BLOCKS", kEdgeBlocks) || edge_items == 0 || interior_items == 0 ||
+      !lds_starts_at_zero(k))
+    return launch(kern, p, lds, std::max(interior_items, edge_items), stream, max_per_cu, xcd,
+                  grid_out);
+  const int grid = grid_for(k, lds, interior_items, max_per_cu);
+  const int resident = cus * resident_per_cu(k, lds, 64);
+  if (grid + static_cast<int>(e) > resident)
+    return launch(kern, p, lds, std::max(interior_items, edge_items), stream, max_per_cu, xcd,
+                  grid_out);
+  p.edge_blocks = e;
+  p.xcd_split = (grid >= 8 && grid % 8 == 0 && env_flag("ECAMD_XCD", xcd)) ? 1u : 0u;
+  if (grid_out) *grid_out = grid;
+  hipLaunchKernelGGL(kern, dim3(grid + static_cast<int>(e)), dim3(kThreadsPerBlock), lds, stream, p);
+  return hipGetLastError();
+}
+
 // Side stream for the small launches of a call (headers, edge items): they
 // write bytes the interior launch does not touch, so they run beside it --
 // forked from and joined back into the caller's stream with events -- and
@@ -1443,10 +1514,11 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   // data fragments are written by the first pass (rows 0..3) only
   const bool data = p.data != nullptr && p.row0 == 0;
   bool probe = false;
-  int per_cu = kEncodePerCu;
+  const int per_cu = env_int("ECAMD_ENC_PER_CU", kEncodePerCu);  // A/B
+  // interior and edge work items (edge items include the headers' objects)
+  const uint32_t edge_items = std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u);
   if constexpr (K == 10 && NR == 4) {
     probe = env_flag("ECAMD_ENC_NOCOMP", false);
-    per_cu = env_int("ECAMD_ENC_PER_CU", kEncodePerCu);  // A/B
     // A/B: CH KiB per wave and slice (ECAMD_ENC_CH=2), nontemporal loads
     // (ECAMD_ENC_NTL=1); plain encode (no CRC, no data fragments) only
     const int ch = env_int("ECAMD_ENC_CH", 1);
@@ -1456,15 +1528,15 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
         !env_flag("ECAMD_EDGE_SIDE", false)) {
       p.fused_edges = 1;
       if (ch == 2) set_tiles(p, room, 2);
-      const uint32_t items = std::max({p.n_obj * p.tiles, p.n_obj * p.edge_tiles,
-                                       p.headers ? p.n_obj : 0u});
+      const uint32_t items = p.n_obj * p.tiles;
+      const uint32_t edges = std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u);
       if (nb == 10)
-        return ntl ? launch(encode_kernel<F, K, NR, false, false, 1, true, 10>, p, lds, items, stream, per_cu)
-                   : launch(encode_kernel<F, K, NR, false, false, 1, false, 10>, p, lds, items, stream, per_cu);
+        return ntl ? launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, true, 10>, p, lds, items, edges, stream, per_cu, true)
+                   : launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, false, 10>, p, lds, items, edges, stream, per_cu, true);
       if (ch == 2)
-        return ntl ? launch(encode_kernel<F, K, NR, false, false, 2, true>, p, lds, items, stream, per_cu)
-                   : launch(encode_kernel<F, K, NR, false, false, 2, false>, p, lds, items, stream, per_cu);
-      return launch(encode_kernel<F, K, NR, false, false, 1, true>, p, lds, items, stream, per_cu);
+        return ntl ? launch_edges_apart(encode_kernel<F, K, NR, false, false, 2, true>, p, lds, items, edges, stream, per_cu, true)
+                   : launch_edges_apart(encode_kernel<F, K, NR, false, false, 2, false>, p, lds, items, edges, stream, per_cu, true);
+      return launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, true>, p, lds, items, edges, stream, per_cu, true);
     }
   }
   hipError_t e;
@@ -1472,22 +1544,21 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     // inline_crc32 with the parity CRC fused: one encode launch + the
     // finishing pass over the run partials
     p.fused_edges = 1;
-    const uint32_t items = std::max({p.n_obj * p.tiles, p.n_obj * p.edge_tiles,
-                                     p.headers ? p.n_obj : 0u});
+    const uint32_t items = p.n_obj * p.tiles;
     int grid = 0;
     const int crc_per_cu = env_int("ECAMD_CRC_PER_CU", kEncodePerCu);  // A/B knob
     bool crc_ntl = false;
     if constexpr (K == 10 && NR == 4) {
       crc_ntl = !data && env_flag("ECAMD_CRC_NTL", false);  // A/B
       if (crc_ntl)
-        e = launch(encode_crc_kernel<F, K, NR, false, true>, p, crc_lds_bytes<F, K>(), items,
-                   stream, crc_per_cu, false, &grid);
+        e = launch_edges_apart(encode_crc_kernel<F, K, NR, false, true>, p, crc_lds_bytes<F, K>(),
+                               items, edge_items, stream, crc_per_cu, false, &grid);
     }
     if (!crc_ntl)
-      e = data ? launch(encode_crc_kernel<F, K, NR, true>, p, crc_lds_bytes<F, K>(), items, stream,
-                        crc_per_cu, false, &grid)
-               : launch(encode_crc_kernel<F, K, NR>, p, crc_lds_bytes<F, K>(), items, stream,
-                        crc_per_cu, false, &grid);
+      e = data ? launch_edges_apart(encode_crc_kernel<F, K, NR, true>, p, crc_lds_bytes<F, K>(),
+                                    items, edge_items, stream, crc_per_cu, false, &grid)
+               : launch_edges_apart(encode_crc_kernel<F, K, NR>, p, crc_lds_bytes<F, K>(), items,
+                                    edge_items, stream, crc_per_cu, false, &grid);
     if (e != hipSuccess) return e;
     CrcFinishParams fp{};
     fp.parity = p.parity;
@@ -1510,13 +1581,18 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     // one launch: interior stream + edge items + headers (+ the data
     // fragments when asked: stored from the input registers)
     p.fused_edges = 1;
-    const uint32_t items = std::max({p.n_obj * p.tiles, p.n_obj * p.edge_tiles,
-                                     p.headers ? p.n_obj : 0u});
+    const uint32_t items = p.n_obj * p.tiles;
     if constexpr (K == 10 && NR == 4)
-      if (probe) return launch(encode_kernel<F, K, NR, true>, p, lds, items, stream, per_cu);
+      if (probe)
+        return env_flag("ECAMD_ENC_NTL", false)
+                   ? launch_edges_apart(encode_kernel<F, K, NR, true, false, 1, true>, p, lds, items,
+                                        edge_items, stream, per_cu, true)
+                   : launch_edges_apart(encode_kernel<F, K, NR, true>, p, lds, items, edge_items,
+                                        stream, per_cu, true);
     if (data && !env_flag("ECAMD_DATA_COPY", false))
-      return launch(encode_kernel<F, K, NR, false, true>, p, lds, items, stream, per_cu);
-    e = launch(encode_kernel<F, K, NR>, p, lds, items, stream, per_cu);
+      return launch_edges_apart(encode_kernel<F, K, NR, false, true>, p, lds, items, edge_items,
+                                stream, per_cu, true);
+    e = launch_edges_apart(encode_kernel<F, K, NR>, p, lds, items, edge_items, stream, per_cu, true);
     if (e != hipSuccess || !data) return e;
     // ECAMD_DATA_COPY=1 (A/B): the data fragments in a copy launch of their own
     return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + kTile - 1) / kTile), stream);
@@ -1580,23 +1656,23 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
     if constexpr (K == 10 && MODE == kDecode) probe = env_flag("ECAMD_DEC_NOCOMP", false);
     if (!env_flag("ECAMD_EDGE_SIDE", false)) {
       p.fused_edges = 1;
-      const uint32_t items = std::max(p.n_obj * p.tiles, edge_items);
-      int per_cu = MODE == kReconstruct ? env_int("ECAMD_REC_PER_CU", kReconstructPerCu)
-                                        : kDecodePerCu;
+      const uint32_t items = p.n_obj * p.tiles;
+      const int per_cu = MODE == kReconstruct ? env_int("ECAMD_REC_PER_CU", kReconstructPerCu)
+                                              : env_int("ECAMD_DEC_PER_CU", kDecodePerCu);  // A/B
       if constexpr (K == 10 && MODE == kDecode) {
-        per_cu = env_int("ECAMD_DEC_PER_CU", kDecodePerCu);  // A/B
         if (probe)
-          return launch(decode_kernel<F, K, MODE, true>, p, lds, items, stream, per_cu,
-                        kDecodeXcd);
+          return launch_edges_apart(decode_kernel<F, K, MODE, true>, p, lds, items, edge_items,
+                                    stream, per_cu, kDecodeXcd);
         const int nb = env_int("ECAMD_DEC_NB", 0);  // A/B: inputs in flight per wave
         if (nb == 10)
-          return launch(decode_kernel<F, K, MODE, false, 10>, p, lds, items, stream, per_cu,
-                        kDecodeXcd);
+          return launch_edges_apart(decode_kernel<F, K, MODE, false, 10>, p, lds, items, edge_items,
+                                    stream, per_cu, kDecodeXcd);
         if (nb == 2)
-          return launch(decode_kernel<F, K, MODE, false, 2>, p, lds, items, stream, per_cu,
-                        kDecodeXcd);
+          return launch_edges_apart(decode_kernel<F, K, MODE, false, 2>, p, lds, items, edge_items,
+                                    stream, per_cu, kDecodeXcd);
       }
-      return launch(decode_kernel<F, K, MODE>, p, lds, items, stream, per_cu, kDecodeXcd);
+      return launch_edges_apart(decode_kernel<F, K, MODE>, p, lds, items, edge_items, stream,
+                                per_cu, kDecodeXcd);
     }
     p.fused_edges = 0;
     return fork_join(

@@ -51,6 +51,15 @@ def main():
     ap.add_argument("--alt", action="store_true",
                     help="alternate encode and decode launches, as bench.py's step does "
                          "(default: each kernel back to back)")
+    ap.add_argument("--ec-type", default="amd_rs_vand",
+                    help="GPU ec_type (isa_l_rs_vand / isa_l_rs_cauchy: GF(2^8) kernels)")
+    ap.add_argument("--crc", action="store_true",
+                    help="inline_crc32 instance (parity CRC fused into the encode launch)")
+    ap.add_argument("--flush-mb", type=int, default=0,
+                    help="with --alt: read-sweep this many MiB of a clean buffer between "
+                         "each decode and the next encode, outside both kernels' events "
+                         "(does the encode's alternation cost go away once the decode's "
+                         "dirty Infinity-Cache lines are evicted by clean reads?)")
     args = ap.parse_args()
 
     import torch
@@ -58,20 +67,22 @@ def main():
 
     k, m, n, B = args.k, args.m, args.obj_bytes, args.batch
     dev = torch.device("cuda:0")
-    bs = batch.blocksize(k, n)
+    bs = batch.blocksize(k, n, batch._CODES[args.ec_type][1])
     stride = (n + 255) // 256 * 256
     gen = torch.Generator(device=dev).manual_seed(20261015)
     objs = torch.randint(0, 256, (B, stride), dtype=torch.uint8, device=dev, generator=gen)
     stripes = batch.stripe_buffer(B, k, m, bs, device=dev)
-    codec = batch.BatchCodec(k, m)
+    codec = batch.BatchCodec(k, m, inline_crc32=args.crc, ec_type=args.ec_type)
     codec.encode(objs, n, parity=stripes[:, k:], data=stripes[:, :k])
     ref_stripes = stripes.clone()
     data = stripes[:, :k] if args.full_stripe else None
     rng = np.random.default_rng(7)
     full = (1 << (k + m)) - 1
-    masks = [full & ~int(sum(1 << int(i) for i in rng.choice(k + m, 4, replace=False)))
+    masks = [full & ~int(sum(1 << int(i) for i in rng.choice(k + m, min(4, m), replace=False)))
              for _ in range(B)]
     out = torch.zeros_like(objs)
+    flush = (torch.ones(args.flush_mb << 18, dtype=torch.int32, device=dev)
+             if args.flush_mb else None)
     enc_bytes = B * (n + (k + m if args.full_stripe else m) * (bs + 80))
     dec_bytes = B * (k * bs + n)
 
@@ -100,19 +111,21 @@ def main():
                 # bench.py's step: encode, decode, encode, ... each kernel
                 # timed by events around it (each pays for the other's
                 # dirty Infinity-Cache lines, as in the bench)
-                ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.reps + 1)]
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(3 * args.reps)]
                 torch.cuda.synchronize()
                 for i in range(args.reps):
-                    ev[2 * i].record()
+                    ev[3 * i].record()
                     codec.encode(objs, n, parity=stripes[:, k:], data=data)
-                    ev[2 * i + 1].record()
+                    ev[3 * i + 1].record()
                     codec.decode(stripes, n, masks, out)
-                ev[2 * args.reps].record()
+                    ev[3 * i + 2].record()
+                    if flush is not None:
+                        flush.sum()
                 torch.cuda.synchronize()
                 times[name]["enc"].append(statistics.mean(
-                    ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(args.reps)) * 1e3)
+                    ev[3 * i].elapsed_time(ev[3 * i + 1]) for i in range(args.reps)) * 1e3)
                 times[name]["dec"].append(statistics.mean(
-                    ev[2 * i + 1].elapsed_time(ev[2 * i + 2]) for i in range(args.reps)) * 1e3)
+                    ev[3 * i + 1].elapsed_time(ev[3 * i + 2]) for i in range(args.reps)) * 1e3)
             else:
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
                 torch.cuda.synchronize()
@@ -132,8 +145,10 @@ def main():
                 out.zero_()
     apply({})
 
-    print(f"k={k} m={m} {B} x {n} B, {args.rounds} rounds x {args.reps} launches, "
-          f"{'alternating encode/decode' if args.alt else 'back to back'}")
+    print(f"{args.ec_type} k={k} m={m} {B} x {n} B, {args.rounds} rounds x {args.reps} launches, "
+          f"{'alternating encode/decode' if args.alt else 'back to back'}"
+          f"{', inline_crc32' if args.crc else ''}"
+          f"{f', {args.flush_mb} MiB clean read sweep before each encode' if flush is not None else ''}")
     print(f"{'variant':<48} {'enc med us':>10} {'min':>8} {'GB/s':>8} "
           f"{'dec med us':>10} {'min':>8} {'GB/s':>8}")
     for name, _ in variants:

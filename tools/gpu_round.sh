@@ -81,7 +81,9 @@ for s in $STEPS; do
     (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run \
       -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-verify --no-host > $O/prof_bench.json 2> $O/prof.err)
     cat $O/prof_bench.json
-    find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \; ;;
+    find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \;
+    [ -f $O/kernel_stats.csv ] || python3 $R/tools/rocpd_stats.py $O/prof $O/kernel_stats.csv > $O/kernel_stats.txt
+    head -12 $O/kernel_stats.txt 2>/dev/null || true ;;
   pmc)
     (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run \
       -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host > $O/pmc_fetch.log 2>&1)
@@ -94,7 +96,7 @@ for s in $STEPS; do
   sq)
     for f in ${SQ_FILES:-pmc1 pmc2 pmc3}; do
       (cd /tmp && timeout -s KILL 150 rocprofv3 -i $R/tools/$f.txt --output-format csv -d $O/sq_$f -o run \
-        -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host > $O/sq_$f.log 2>&1)
+        -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host ${SQ_ARGS:-} > $O/sq_$f.log 2>&1)
     done
     python3 $R/tools/pmc_table.py $(for f in ${SQ_FILES:-pmc1 pmc2 pmc3}; do echo $O/sq_$f; done) > $O/sq_table.txt 2>&1 || true
     cat $O/sq_table.txt ;;

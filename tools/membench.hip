@@ -15,6 +15,7 @@
 // buffer by 2.85 MB: its stripes were sized for a different object count).
 //
 //   ./membench [reps] [sections]     sections: any of "base enc dec alt" (default all)
+//   MB_RANDOM=1: random object bytes instead of a constant fill
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -458,6 +459,19 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&frags_raw, frag_bytes));
   CHECK(hipMalloc(&sink, 64));
   CHECK(hipMemset(objs, 1, obj_bytes));
+  if (const char* r = std::getenv("MB_RANDOM"); r != nullptr && r[0] == '1') {
+    // random object bytes, as bench.py's (the constant fill flips no bus bits)
+    std::vector<uint64_t> host(obj_bytes / 8);
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (auto& v : host) {
+      x ^= x << 13;
+      x ^= x >> 7;
+      x ^= x << 17;
+      v = x;
+    }
+    CHECK(hipMemcpy(objs, host.data(), host.size() * 8, hipMemcpyHostToDevice));
+    std::printf("random object bytes\n");
+  }
   CHECK(hipMemset(out, 0, obj_bytes));
   CHECK(hipMemset(frags_raw, 2, frag_bytes));
   uint8_t* frags = frags_raw + 48;  // payloads (80 B past each fragment start) 128-B aligned
