@@ -92,6 +92,11 @@ def parse(argv=None):
     ap.add_argument("--no-host", action="store_true",
                     help="skip the host-resident (pinned H2D/D2H) encode/decode timing")
     ap.add_argument("--host", action="store_true", help=argparse.SUPPRESS)  # always on now
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="before the --warmup steps, run untimed steps for this long so the "
+                         "GPU reaches its steady clocks (the kernel times fall by up to 25 %% "
+                         "over the first ~20 ms of load: profiles/r03q_bench_*.json step_ms); "
+                         "0 = off.  Reported as `settle` in the JSON line")
     ap.add_argument("--fresh-steps", type=int, default=8,
                     help="decode steps whose erasure masks are new every step (drawn from "
                          "the seed outside the clock, handed over inside it): timed apart "
@@ -664,6 +669,21 @@ def main():
         else:
             codec.reconstruct(stripes, n, rmasks, dests, rec)
 
+    # Clock settle, then the W warmup steps.  A fresh box starts the step
+    # below its steady clocks and the kernels speed up over the first ~20 ms
+    # of sustained load (r03q, --inline-crc32: encode 528 us in the first
+    # timed step after 5 warmup steps, 360 us twenty steps later; 373 -> 340
+    # after 30 warmup steps), so the timed steps would measure the ramp, not
+    # the path.  The settle steps are the same untimed work as the warmup
+    # steps, bounded by time, and reported.
+    settle_steps, t_settle = 0, time.perf_counter()
+    while args.settle_ms > 0 and (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        step()
+        settle_steps += 1
+        if settle_steps % 8 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    settle_ms = (time.perf_counter() - t_settle) * 1e3 if settle_steps else 0.0
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -756,6 +776,13 @@ def main():
         f"{two}_GiBps": round(n_total * n / (dec_ms * 1e-3) / 2**30, 3),
         "kernels": kernels,
         "roofline": roofline,
+        "settle": {"ms": round(settle_ms, 1), "steps": settle_steps,
+                   "note": "untimed steps before the warmup steps, until the GPU's clocks "
+                           "settle (--settle-ms)"},
+        "step_ms": {"encode": [round(events[2 * i].elapsed_time(events[2 * i + 1]), 4)
+                               for i in range(args.steps)],
+                    two: [round(events[2 * i + 1].elapsed_time(events[2 * i + 2]), 4)
+                          for i in range(args.steps)]},
     }
     if args.same_device and world > 1:
         result["same_device"] = True

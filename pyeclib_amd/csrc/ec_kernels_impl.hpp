@@ -584,7 +584,7 @@ __host__ __device__ constexpr int stream_slots() {
 //     (launch_edges_apart; round 3, profiles/r03g_ab_alt.txt: 283.2 us at 2
 //     vs 305.8 at 8; at 2 with the edges in front of interior blocks
 //     301.7).  2 is also the best of 2/3/4/8 for k = 2, 4, 6, 7, 8, 12, for
-//     k = 4 m = 2 and for the GF(2^8) codes (profiles/r03h_ab_k*.txt), and
+//     k = 4 m = 2 and for the GF(2^8) codes (profiles/r03h_ab_per_cu_by_k.txt), and
 //     for the fused-CRC encode (339.7 vs 362.6 us at 8).
 constexpr int kEncodeOcc = 8, kEncodePerCu = 2;
 // The fused-CRC encode's register budget: 7 waves per SIMD (72 VGPRs, no
@@ -593,6 +593,12 @@ constexpr int kEncodeOcc = 8, kEncodePerCu = 2;
 // 30: 72 VGPRs spilled 8-36 B); the full-stripe form (data fragments stored
 // too) keeps 5.
 constexpr int kEncodeCrcOcc = 7, kEncodeCrcDataOcc = 5;
+// (Round 3 also measured the fused-CRC encode walking runs of R interior
+// tiles dealt grid-stride, XCD-major -- a compact footprint like the plain
+// encode's -- with a block join per run: 371.3 us at R = 8, 418.4 at 4,
+// 387.7 at 16, against 342.7 for one contiguous range per block
+// (profiles/r03l_ab_crc.txt).  The per-run joins cost more than the order
+// gains; not kept.)
 // Full-stripe encode (data fragments stored too): no register cap.  Capped
 // at 64 VGPRs the edge items' extra stores spilled (44 B per lane of
 // scratch), and hipcc still spilled 12 B at a 72 cap; uncapped it takes 70

@@ -55,6 +55,9 @@ def main():
                     help="GPU ec_type (isa_l_rs_vand / isa_l_rs_cauchy: GF(2^8) kernels)")
     ap.add_argument("--crc", action="store_true",
                     help="inline_crc32 instance (parity CRC fused into the encode launch)")
+    ap.add_argument("--bench-alloc", action="store_true",
+                    help="objects made as bench.py makes them (PCG64 bytes in host memory, "
+                         "copied to the GPU) and its reconstruct buffer allocated too")
     ap.add_argument("--flush-mb", type=int, default=0,
                     help="with --alt: read-sweep this many MiB of a clean buffer between "
                          "each decode and the next encode, outside both kernels' events "
@@ -69,8 +72,15 @@ def main():
     dev = torch.device("cuda:0")
     bs = batch.blocksize(k, n, batch._CODES[args.ec_type][1])
     stride = (n + 255) // 256 * 256
-    gen = torch.Generator(device=dev).manual_seed(20261015)
-    objs = torch.randint(0, 256, (B, stride), dtype=torch.uint8, device=dev, generator=gen)
+    if args.bench_alloc:
+        host = np.zeros((B, stride), dtype=np.uint8)
+        host[:, :n] = np.random.Generator(np.random.PCG64(20261015)).integers(
+            0, 256, size=(B, n), dtype=np.uint8)
+        objs = torch.from_numpy(host).to(dev)
+        del host
+    else:
+        gen = torch.Generator(device=dev).manual_seed(20261015)
+        objs = torch.randint(0, 256, (B, stride), dtype=torch.uint8, device=dev, generator=gen)
     stripes = batch.stripe_buffer(B, k, m, bs, device=dev)
     codec = batch.BatchCodec(k, m, inline_crc32=args.crc, ec_type=args.ec_type)
     codec.encode(objs, n, parity=stripes[:, k:], data=stripes[:, :k])
@@ -81,6 +91,8 @@ def main():
     masks = [full & ~int(sum(1 << int(i) for i in rng.choice(k + m, min(4, m), replace=False)))
              for _ in range(B)]
     out = torch.zeros_like(objs)
+    if args.bench_alloc:
+        rec = torch.zeros((B, batch.frag_stride(bs)), dtype=torch.uint8, device=dev)  # noqa: F841
     flush = (torch.ones(args.flush_mb << 18, dtype=torch.int32, device=dev)
              if args.flush_mb else None)
     enc_bytes = B * (n + (k + m if args.full_stripe else m) * (bs + 80))

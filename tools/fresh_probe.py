@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Where a decode with new erasure masks spends its time (dev tool): the host
+call (enqueue) time and the GPU event span, for masks drawn anew per call
+against the same masks repeated, at bench.py's workload (k=10 m=4,
+256 x 4 MiB)."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    from pyeclib_amd import batch
+    k, m, n, B = 10, 4, 4 << 20, 256
+    dev = torch.device("cuda:0")
+    bs = batch.blocksize(k, n)
+    objs = torch.randint(0, 256, (B, n), dtype=torch.uint8, device=dev)
+    stripes = batch.stripe_buffer(B, k, m, bs, device=dev)
+    codec = batch.BatchCodec(k, m)
+    codec.encode(objs, n, parity=stripes[:, k:], data=stripes[:, :k])
+    out = torch.zeros_like(objs)
+    full = (1 << (k + m)) - 1
+
+    def masks(seed):
+        rng = np.random.default_rng(seed)
+        return [full & ~int(sum(1 << int(i) for i in rng.choice(k + m, 4, replace=False)))
+                for _ in range(B)]
+
+    for label, seeds in (("fresh", range(100, 112)), ("repeat", [7] * 12)):
+        host_us, span_us = [], []
+        for s in seeds:
+            mk = masks(s)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record()
+            codec.decode(stripes, n, mk, out)
+            t1 = time.perf_counter()
+            e1.record()
+            torch.cuda.synchronize()
+            host_us.append((t1 - t0) * 1e6)
+            span_us.append(e0.elapsed_time(e1) * 1e3)
+        print(f"{label:7s} host call median {np.median(host_us[2:]):8.1f} us  "
+              f"event span median {np.median(span_us[2:]):8.1f} us  (first {host_us[0]:.0f} / {span_us[0]:.0f})")
+        assert torch.equal(out, objs)
+
+
+if __name__ == "__main__":
+    main()

@@ -67,7 +67,7 @@ for s in $STEPS; do
     (cd $R && timeout -k 10 400 python3 tools/swift_mix.py > $O/swift_mix.json 2> $O/swift_mix.err)
     head -c 400 $O/swift_mix.json ;;
   crc)
-    (cd $R && timeout -k 10 300 python3 bench.py --inline-crc32 --steps 10 --no-host \
+    (cd $R && timeout -k 10 300 python3 bench.py --inline-crc32 --steps 20 --warmup 5 --no-host \
         --no-cpu-baseline > $O/bench_crc.json 2> $O/bench_crc.err)
     tail -c 400 $O/bench_crc.json ;;
   crcntl)
@@ -75,7 +75,7 @@ for s in $STEPS; do
         --no-cpu-baseline > $O/bench_crc_ntl.json 2> $O/bench_crc_ntl.err)
     tail -c 400 $O/bench_crc_ntl.json ;;
   bench)
-    (cd $R && timeout -k 10 400 python3 bench.py > $O/bench.json 2> $O/bench.err)
+    (cd $R && timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err)
     cat $O/bench.json ;;
   prof)
     (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run \

@@ -14,7 +14,7 @@
 // its first launch (round 2's compact-layout probe overran the fragment
 // buffer by 2.85 MB: its stripes were sized for a different object count).
 //
-//   ./membench [reps] [sections]     sections: any of "base enc dec alt" (default all)
+//   ./membench [reps] [sections]     sections: any of "base enc ceil runs dec alt" (default all)
 //   MB_RANDOM=1: random object bytes instead of a constant fill
 #include <hip/hip_runtime.h>
 
@@ -300,8 +300,9 @@ __device__ __forceinline__ Rsrc mk_rsrc(const void* base, int records = -1) {
   return __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, n, 0x00020000);
 }
-template <int CH, int NB, int ORD, bool NTL, bool ST_NOP>
-__global__ void __launch_bounds__(256) enc_stream_buf_kernel(Shape s) {
+template <int CH, int NB, int ORD, bool NTL, bool ST_NOP, int OCC = 1>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8)))
+    enc_stream_buf_kernel(Shape s) {
   constexpr int SL = K * CH;  // slots per item
   const Order r = order<ORD>(s.n_obj * s.tiles, s.tiles);
   uint32_t w = r.begin;
@@ -345,6 +346,59 @@ __global__ void __launch_bounds__(256) enc_stream_buf_kernel(Shape s) {
         }
         acc = v4u{0u, 0u, 0u, 0u};
       }
+    }
+    if (wn == w) break;
+    w = wn;
+    x = xn;
+    cur = nxt;
+  }
+}
+
+// The buf-stream encode in "runs": block b takes runs b, b + G, ... of RUN
+// consecutive items (the order a per-thread Horner CRC over RUN tiles of one
+// payload needs; RUN = 1 is the plain grid-stride order).
+template <int RUN, bool NTL>
+__global__ void __launch_bounds__(256) enc_stream_run_kernel(Shape s) {
+  constexpr int NB = 5, SL = K;
+  const uint32_t items = s.n_obj * s.tiles;
+  const uint32_t G = gridDim.x;
+  uint32_t w = blockIdx.x * RUN;
+  if (w >= items) return;
+  auto next = [&](uint32_t it) -> uint32_t {
+    const uint32_t n = (it % RUN == RUN - 1) ? it + 1 + (G - 1) * RUN : it + 1;
+    return n < items ? n : it;
+  };
+  const uint32_t lane16 = (threadIdx.x & 63) * 16;
+  const uint32_t wx = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * 1024);
+  auto item_x = [&](uint32_t it) { return (it - it / s.tiles * s.tiles) * 4096 + wx; };
+  auto obj_of = [&](uint32_t it, int rec) { return mk_rsrc(s.objs + (it / s.tiles) * s.obj_stride, rec); };
+  Rsrc cur = obj_of(w, -1);
+  uint32_t x = item_x(w);
+  v4u buf[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+    buf[i] = __builtin_amdgcn_raw_buffer_load_b128(cur, lane16, i * s.bs + x, NTL ? 2 : 0);
+  while (true) {
+    const uint32_t wn = next(w);
+    const Rsrc nxt = obj_of(wn, wn == w ? 0 : -1);
+    const uint32_t xn = item_x(wn);
+    const Rsrc par = mk_rsrc(s.frags + (w / s.tiles) * s.stripe_stride);
+    v4u acc = v4u{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < SL; ++i) {
+      acc ^= buf[i % NB];
+      if (i + NB < SL)
+        buf[i % NB] = __builtin_amdgcn_raw_buffer_load_b128(cur, lane16, (i + NB) * s.bs + x, NTL ? 2 : 0);
+      else
+        buf[i % NB] = __builtin_amdgcn_raw_buffer_load_b128(nxt, lane16, (i + NB - SL) * s.bs + xn, NTL ? 2 : 0);
+    }
+#pragma unroll
+    for (int q = 0; q < M; ++q) {
+      __builtin_amdgcn_raw_buffer_store_b128(acc + uint32_t(q), par, lane16,
+                                             uint32_t(K + q) * uint32_t(s.frag_stride) + 80 + x, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 0");
+      __builtin_amdgcn_sched_barrier(0);
     }
     if (wn == w) break;
     w = wn;
@@ -497,6 +551,47 @@ int main(int argc, char** argv) {
   }
   Shape s{objs, frags, bs_real, n_obj, bs_real / 4096, obj_stride, fs, ss};
   const double enc_bytes = double(n_obj) * s.tiles * 4096 * (K + M);
+    // run orders (the fused-CRC encode's candidates): runs of R items per block
+  // the encode pattern's ceiling rows only (same kernels as "enc")
+  if (want(sections, "ceil")) {
+    for (int bpc : {1, 2, 3, 4}) {
+      const int grid = g_cus * bpc;
+      Shape s2 = s;
+      s2.tiles = bs_real / 8192;
+      const double b1 = double(n_obj) * s.tiles * 4096 * (K + M);
+      const double b2 = double(n_obj) * s2.tiles * 8192 * (K + M);
+      report("enc buf-stream CH1 NB5 xcd (product)", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 5, 1, false, true><<<grid, 256>>>(s); }), b1);
+      report("enc buf-stream CH1 NB5 xcd ld-nt", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 5, 1, true, true><<<grid, 256>>>(s); }), b1);
+      report("enc CH2 ld-nt", bpc, time_us([&] { enc_kernel<2, true, true, false><<<grid, 256>>>(s2); }), b2);
+      report("enc buf-stream CH1 NB5 xcd, product budget (8 waves/SIMD) + 5 KiB LDS", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 5, 1, false, true, 8><<<grid, 256, 5120>>>(s); }), b1);
+      report("enc buf-stream CH1 NB5 xcd + 5 KiB LDS", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 5, 1, false, true><<<grid, 256, 5120>>>(s); }), b1);
+      report("enc buf-stream CH1 NB5 xcd, product budget", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 5, 1, false, true, 8><<<grid, 256>>>(s); }), b1);
+      report("enc buf-stream CH1 NB2 xcd ld-nt", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 2, 1, true, true><<<grid, 256>>>(s); }), b1);
+      report("enc buf-stream CH1 NB2 xcd", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 2, 1, false, true><<<grid, 256>>>(s); }), b1);
+    }
+  }
+  if (want(sections, "runs")) {
+    for (int bpc : {2, 4}) {
+      const int grid = g_cus * bpc;
+      const double b1 = double(n_obj) * s.tiles * 4096 * (K + M);
+      report("enc runs R1 (grid-stride)", bpc, time_us([&] { enc_stream_run_kernel<1, false><<<grid, 256>>>(s); }), b1);
+      report("enc runs R2", bpc, time_us([&] { enc_stream_run_kernel<2, false><<<grid, 256>>>(s); }), b1);
+      report("enc runs R4", bpc, time_us([&] { enc_stream_run_kernel<4, false><<<grid, 256>>>(s); }), b1);
+      report("enc runs R8", bpc, time_us([&] { enc_stream_run_kernel<8, false><<<grid, 256>>>(s); }), b1);
+      report("enc runs R16", bpc, time_us([&] { enc_stream_run_kernel<16, false><<<grid, 256>>>(s); }), b1);
+      report("enc runs R32", bpc, time_us([&] { enc_stream_run_kernel<32, false><<<grid, 256>>>(s); }), b1);
+      report("enc runs R8 ld-nt", bpc, time_us([&] { enc_stream_run_kernel<8, true><<<grid, 256>>>(s); }), b1);
+      report("enc buf-stream block ranges (CRC order)", bpc,
+             time_us([&] { enc_stream_buf_kernel<1, 5, 3, false, true><<<grid, 256>>>(s); }), b1);
+    }
+  }
   if (want(sections, "enc")) {
     // the 10:4 encode mix split into its halves
     check_shape("enc halves", s, 4096);
