@@ -586,6 +586,11 @@ __host__ __device__ constexpr int stream_slots() {
 //     301.7).  2 is also the best of 2/3/4/8 for k = 2, 4, 6, 7, 8, 12, for
 //     k = 4 m = 2 and for the GF(2^8) codes (profiles/r03h_ab_per_cu_by_k.txt), and
 //     for the fused-CRC encode (339.7 vs 362.6 us at 8).
+// (Measured round 3 and not kept: all 32 lookups of an input -- and of a CRC
+// row -- issued before their XORs, one LDS round trip per input instead of
+// four, at a 2-wave budget: encode 297.7 vs 284.6 us, fused-CRC encode 350.8
+// vs 353.6; profiles/r03s_ab_*.txt.  The lookup latency is not what the
+// 2-per-CU launch waits on.)
 constexpr int kEncodeOcc = 8, kEncodePerCu = 2;
 // The fused-CRC encode's register budget: 7 waves per SIMD (72 VGPRs, no
 // scratch at k = 10, m = 4) once its item range stopped feeding waterfall
@@ -606,9 +611,12 @@ constexpr int kEncodeCrcOcc = 7, kEncodeCrcDataOcc = 5;
 // kernel's actual register count (resident_per_cu).
 constexpr int kEncodeDataOcc = 1;
 constexpr int kDecodeOcc = 4, kDecodePerCu = 2;
-// Reconstruct (k reads, one row written) keeps 4 per CU: at 2 the config-3
-// reconstruct (GF(2^8), k = 12, 16 MiB) ran 0.586 ms vs 0.500 before.
-constexpr int kReconstructPerCu = 4;
+// Reconstruct (k reads, one row written): 2 per CU since its edge items run
+// in blocks of their own (round 3, config 3: GF(2^8) k = 12, 128 x 16 MiB,
+// bench.py --second reconstruct: 448.0 us at 2, 451.7 at 3, 477.4 at 4,
+// 476.9 at 6; profiles/r03t_config3_rec*.json).  Round 2, with the edges in
+// front of interior blocks, measured 0.586 ms at 2 vs 0.500 at 4.
+constexpr int kReconstructPerCu = 2;
 // Decode walks its items without the XCD-major split (grid-stride over the
 // whole list): measured round 2, same process, three boxes: 437.0 vs 446.1,
 // 438.8 vs 445.6, 436.5 vs 444.3 us.  Encode is indifferent (+-0.3 us) and
