@@ -14,7 +14,7 @@
 // its first launch (round 2's compact-layout probe overran the fragment
 // buffer by 2.85 MB: its stripes were sized for a different object count).
 //
-//   ./membench [reps] [sections]     sections: any of "base enc ceil runs dec alt" (default all)
+//   ./membench [reps] [sections]     sections: any of "base enc ceil wpb runs dec alt" (default all)
 //   MB_RANDOM=1: random object bytes instead of a constant fill
 #include <hip/hip_runtime.h>
 
@@ -407,6 +407,61 @@ __global__ void __launch_bounds__(256) enc_stream_run_kernel(Shape s) {
   }
 }
 
+// The product stream with WPB waves per block (WPB x 64 threads): an item is
+// WPB KiB of payload positions, one 1 KiB chunk per wave.  Do 1 block of 8
+// waves per CU behave like 1 block of 4 (fewer, larger blocks) or like 2
+// blocks of 4 (the same waves)?
+template <int WPB, bool NTL>
+__global__ void __launch_bounds__(WPB * 64) enc_stream_wpb_kernel(Shape s) {
+  constexpr int NB = 5, SL = K;
+  constexpr uint32_t T = WPB * 1024u;
+  const uint32_t tiles = s.bs / T;
+  const uint32_t items = s.n_obj * tiles;
+  // XCD-major split as order<1>
+  const uint32_t xg = blockIdx.x & 7u;
+  const uint32_t lo = uint32_t(uint64_t(items) * xg / 8), hi = uint32_t(uint64_t(items) * (xg + 1) / 8);
+  uint32_t w = lo + (blockIdx.x >> 3);
+  const uint32_t step = gridDim.x >> 3;
+  if (w >= hi) return;
+  const uint32_t lane16 = (threadIdx.x & 63) * 16;
+  const uint32_t wx = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * 1024);
+  auto item_x = [&](uint32_t it) { return (it - it / tiles * tiles) * T + wx; };
+  auto obj_of = [&](uint32_t it, int rec) { return mk_rsrc(s.objs + (it / tiles) * s.obj_stride, rec); };
+  Rsrc cur = obj_of(w, -1);
+  uint32_t x = item_x(w);
+  v4u buf[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+    buf[i] = __builtin_amdgcn_raw_buffer_load_b128(cur, lane16, i * s.bs + x, NTL ? 2 : 0);
+  while (true) {
+    const uint32_t wn = w + step < hi ? w + step : w;
+    const Rsrc nxt = obj_of(wn, wn == w ? 0 : -1);
+    const uint32_t xn = item_x(wn);
+    const Rsrc par = mk_rsrc(s.frags + (w / tiles) * s.stripe_stride);
+    v4u acc = v4u{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < SL; ++i) {
+      acc ^= buf[i % NB];
+      if (i + NB < SL)
+        buf[i % NB] = __builtin_amdgcn_raw_buffer_load_b128(cur, lane16, (i + NB) * s.bs + x, NTL ? 2 : 0);
+      else
+        buf[i % NB] = __builtin_amdgcn_raw_buffer_load_b128(nxt, lane16, (i + NB - SL) * s.bs + xn, NTL ? 2 : 0);
+    }
+#pragma unroll
+    for (int q = 0; q < M; ++q) {
+      __builtin_amdgcn_raw_buffer_store_b128(acc + uint32_t(q), par, lane16,
+                                             uint32_t(K + q) * uint32_t(s.frag_stride) + 80 + x, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 0");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (wn == w) break;
+    w = wn;
+    x = xn;
+    cur = nxt;
+  }
+}
+
 // ---- decode stream: read the 10 data-fragment payloads (line-aligned),
 // write them to the object's slices at j*bs + x. ----
 template <bool NTL, bool NTS>
@@ -575,6 +630,29 @@ int main(int argc, char** argv) {
              time_us([&] { enc_stream_buf_kernel<1, 2, 1, true, true><<<grid, 256>>>(s); }), b1);
       report("enc buf-stream CH1 NB2 xcd", bpc,
              time_us([&] { enc_stream_buf_kernel<1, 2, 1, false, true><<<grid, 256>>>(s); }), b1);
+    }
+  }
+  // waves per block: 1 x 8-wave blocks vs 2 x 4-wave blocks per CU
+  if (want(sections, "wpb")) {
+    const double b4 = double(n_obj) * (bs_real / 4096) * 4096 * (K + M);
+    const double b8 = double(n_obj) * (bs_real / 8192) * 8192 * (K + M);
+    for (int ntl = 0; ntl < 2; ++ntl) {
+      auto r4 = [&](int bpc) {
+        return time_us([&] {
+          if (ntl) enc_stream_wpb_kernel<4, true><<<g_cus * bpc, 256>>>(s);
+          else enc_stream_wpb_kernel<4, false><<<g_cus * bpc, 256>>>(s);
+        });
+      };
+      auto r8 = [&](int bpc) {
+        return time_us([&] {
+          if (ntl) enc_stream_wpb_kernel<8, true><<<g_cus * bpc, 512>>>(s);
+          else enc_stream_wpb_kernel<8, false><<<g_cus * bpc, 512>>>(s);
+        });
+      };
+      report(ntl ? "enc wpb4 ld-nt" : "enc wpb4", 1, r4(1), b4);
+      report(ntl ? "enc wpb4 ld-nt" : "enc wpb4", 2, r4(2), b4);
+      report(ntl ? "enc wpb8 ld-nt" : "enc wpb8", 1, r8(1), b8);
+      report(ntl ? "enc wpb8 ld-nt" : "enc wpb8", 2, r8(2), b8);
     }
   }
   if (want(sections, "runs")) {
