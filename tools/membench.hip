@@ -411,10 +411,15 @@ __global__ void __launch_bounds__(256) enc_stream_run_kernel(Shape s) {
 // WPB KiB of payload positions, one 1 KiB chunk per wave.  Do 1 block of 8
 // waves per CU behave like 1 block of 4 (fewer, larger blocks) or like 2
 // blocks of 4 (the same waves)?
-template <int WPB, bool NTL>
+// SPREAD: consecutive items of a block alternate between the two halves of
+// its XCD range (the footprint in flight doubles at the same wave count).
+// HALF: each wave moves 512 B per chunk (lanes 0-31), an item WPB x 512 B.
+template <int WPB, bool NTL, bool SPREAD = false, bool HALF = false>
 __global__ void __launch_bounds__(WPB * 64) enc_stream_wpb_kernel(Shape s) {
   constexpr int NB = 5, SL = K;
-  constexpr uint32_t T = WPB * 1024u;
+  constexpr uint32_t CB = HALF ? 512u : 1024u;
+  constexpr uint32_t T = WPB * CB;
+  if (HALF && (threadIdx.x & 63) >= 32) return;
   const uint32_t tiles = s.bs / T;
   const uint32_t items = s.n_obj * tiles;
   // XCD-major split as order<1>
@@ -424,9 +429,17 @@ __global__ void __launch_bounds__(WPB * 64) enc_stream_wpb_kernel(Shape s) {
   const uint32_t step = gridDim.x >> 3;
   if (w >= hi) return;
   const uint32_t lane16 = (threadIdx.x & 63) * 16;
-  const uint32_t wx = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * 1024);
-  auto item_x = [&](uint32_t it) { return (it - it / tiles * tiles) * T + wx; };
-  auto obj_of = [&](uint32_t it, int rec) { return mk_rsrc(s.objs + (it / tiles) * s.obj_stride, rec); };
+  const uint32_t wx = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * CB);
+  const uint32_t half = (hi - lo) / 2;
+  auto real = [&](uint32_t v) {
+    if (!SPREAD) return v;
+    const uint32_t d = v - lo;
+    return (d & 1u) ? lo + half + d / 2 : lo + d / 2;
+  };
+  auto item_x = [&](uint32_t it) { it = real(it); return (it - it / tiles * tiles) * T + wx; };
+  auto obj_of = [&](uint32_t it, int rec) {
+    return mk_rsrc(s.objs + (real(it) / tiles) * s.obj_stride, rec);
+  };
   Rsrc cur = obj_of(w, -1);
   uint32_t x = item_x(w);
   v4u buf[NB];
@@ -437,7 +450,7 @@ __global__ void __launch_bounds__(WPB * 64) enc_stream_wpb_kernel(Shape s) {
     const uint32_t wn = w + step < hi ? w + step : w;
     const Rsrc nxt = obj_of(wn, wn == w ? 0 : -1);
     const uint32_t xn = item_x(wn);
-    const Rsrc par = mk_rsrc(s.frags + (w / tiles) * s.stripe_stride);
+    const Rsrc par = mk_rsrc(s.frags + (real(w) / tiles) * s.stripe_stride);
     v4u acc = v4u{0u, 0u, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < SL; ++i) {
@@ -654,6 +667,16 @@ int main(int argc, char** argv) {
       report(ntl ? "enc wpb8 ld-nt" : "enc wpb8", 1, r8(1), b8);
       report(ntl ? "enc wpb8 ld-nt" : "enc wpb8", 2, r8(2), b8);
     }
+    // footprint vs wave count (nontemporal loads)
+    const double b2 = double(n_obj) * (bs_real / 2048) * 2048 * (K + M);
+    report("enc wpb4 ld-nt SPREAD (2x footprint, 4 waves/CU)", 1,
+           time_us([&] { enc_stream_wpb_kernel<4, true, true><<<g_cus, 256>>>(s); }), b4);
+    report("enc wpb4 ld-nt HALF (512 B/wave, 4 waves/CU)", 1,
+           time_us([&] { enc_stream_wpb_kernel<4, true, false, true><<<g_cus, 256>>>(s); }), b2);
+    report("enc wpb4 ld-nt HALF (512 B/wave, 8 waves/CU)", 2,
+           time_us([&] { enc_stream_wpb_kernel<4, true, false, true><<<g_cus * 2, 256>>>(s); }), b2);
+    report("enc wpb8 ld-nt HALF (512 B/wave, 8 waves/CU)", 1,
+           time_us([&] { enc_stream_wpb_kernel<8, true, false, true><<<g_cus, 512>>>(s); }), b4);
   }
   if (want(sections, "runs")) {
     for (int bpc : {2, 4}) {
