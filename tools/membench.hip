@@ -475,6 +475,64 @@ __global__ void __launch_bounds__(WPB * 64) enc_stream_wpb_kernel(Shape s) {
   }
 }
 
+// Paired slices: lanes 0-31 read slice 2i and lanes 32-63 slice 2i+1 at the
+// same 512 B of positions, so each load instruction moves two 512-B
+// segments; a wave's chunk is 512 B of positions, an item 4 x 512 B.  NP
+// pairs in flight per wave.  Parity rows 0-1 stored by lanes 0-31 and 2-3 by
+// lanes 32-63 (as the real kernel would after a 32-lane swap).
+template <int NP, bool NTL>
+__global__ void __launch_bounds__(256) enc_pair_kernel(Shape s) {
+  constexpr int SL = K / 2;  // pair slots per item
+  constexpr uint32_t T = 4 * 512u;
+  const uint32_t tiles = s.bs / T;
+  const uint32_t items = s.n_obj * tiles;
+  const uint32_t xg = blockIdx.x & 7u;
+  const uint32_t lo = uint32_t(uint64_t(items) * xg / 8), hi = uint32_t(uint64_t(items) * (xg + 1) / 8);
+  uint32_t w = lo + (blockIdx.x >> 3);
+  const uint32_t step = gridDim.x >> 3;
+  if (w >= hi) return;
+  const uint32_t l = threadIdx.x & 63;
+  const uint32_t hl = l >> 5;                  // 0: even slice, 1: odd slice
+  const uint32_t voff = (l & 31) * 16 + hl * s.bs;
+  const uint32_t wx = __builtin_amdgcn_readfirstlane((threadIdx.x >> 6) * 512);
+  auto item_x = [&](uint32_t it) { return (it - it / tiles * tiles) * T + wx; };
+  auto obj_of = [&](uint32_t it, int rec) { return mk_rsrc(s.objs + (it / tiles) * s.obj_stride, rec); };
+  Rsrc cur = obj_of(w, -1);
+  uint32_t x = item_x(w);
+  v4u buf[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i)
+    buf[i] = __builtin_amdgcn_raw_buffer_load_b128(cur, voff, 2 * i * s.bs + x, NTL ? 2 : 0);
+  while (true) {
+    const uint32_t wn = w + step < hi ? w + step : w;
+    const Rsrc nxt = obj_of(wn, wn == w ? 0 : -1);
+    const uint32_t xn = item_x(wn);
+    const Rsrc par = mk_rsrc(s.frags + (w / tiles) * s.stripe_stride);
+    v4u acc = v4u{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < SL; ++i) {
+      acc ^= buf[i % NP];
+      if (i + NP < SL)
+        buf[i % NP] = __builtin_amdgcn_raw_buffer_load_b128(cur, voff, 2 * (i + NP) * s.bs + x, NTL ? 2 : 0);
+      else
+        buf[i % NP] = __builtin_amdgcn_raw_buffer_load_b128(nxt, voff, 2 * (i + NP - SL) * s.bs + xn, NTL ? 2 : 0);
+    }
+    const uint32_t soff_lane = (l & 31) * 16 + hl * 2 * uint32_t(s.frag_stride);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      __builtin_amdgcn_raw_buffer_store_b128(acc + uint32_t(q), par, soff_lane,
+                                             uint32_t(K + q) * uint32_t(s.frag_stride) + 80 + x, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 0");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (wn == w) break;
+    w = wn;
+    x = xn;
+    cur = nxt;
+  }
+}
+
 // ---- decode stream: read the 10 data-fragment payloads (line-aligned),
 // write them to the object's slices at j*bs + x. ----
 template <bool NTL, bool NTS>
@@ -676,7 +734,15 @@ int main(int argc, char** argv) {
     report("enc wpb4 ld-nt HALF (512 B/wave, 8 waves/CU)", 2,
            time_us([&] { enc_stream_wpb_kernel<4, true, false, true><<<g_cus * 2, 256>>>(s); }), b2);
     report("enc wpb8 ld-nt HALF (512 B/wave, 8 waves/CU)", 1,
-           time_us([&] { enc_stream_wpb_kernel<8, true, false, true><<<g_cus, 512>>>(s); }), b4);
+           time_us([&] { enc_stream_wpb_kernel<8, true, false, true><<<g_cus, 512>>>(s); }), b4);    const double bp = double(n_obj) * (bs_real / 2048) * 2048 * (K + M);
+    for (int bpc : {1, 2, 3}) {
+      report("enc pairs NP5 ld-nt (2 x 512 B per load)", bpc,
+             time_us([&] { enc_pair_kernel<5, true><<<g_cus * bpc, 256>>>(s); }), bp);
+      report("enc pairs NP5 (2 x 512 B per load)", bpc,
+             time_us([&] { enc_pair_kernel<5, false><<<g_cus * bpc, 256>>>(s); }), bp);
+      report("enc pairs NP3 ld-nt", bpc,
+             time_us([&] { enc_pair_kernel<3, true><<<g_cus * bpc, 256>>>(s); }), bp);
+    }
   }
   if (want(sections, "runs")) {
     for (int bpc : {2, 4}) {
