@@ -42,7 +42,10 @@
 #include <cstdlib>
 #include <cstddef>
 #include <type_traits>
+#include <atomic>
+#include <map>
 #include <mutex>
+#include <utility>
 #include <unordered_map>
 
 #include "crc32.hpp"
@@ -1365,23 +1368,50 @@ inline bool env_flag(const char* name, bool dflt) {
 // (MI355X_MICROARCH.md, Residency), and a grid-stride kernel must not queue
 // blocks behind the resident ones -- and by `max_per_cu`.
 inline int resident_per_cu(const void* kernel, size_t lds_bytes, int max_per_cu) {
-  int per_cu = max_per_cu;
-  int b = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kThreadsPerBlock, lds_bytes) ==
-          hipSuccess &&
-      b > 0)
-    per_cu = std::min(per_cu, b);
-  hipFuncAttributes attr{};
-  if (hipFuncGetAttributes(&attr, kernel) == hipSuccess && attr.numRegs > 0)
-    per_cu = std::min(per_cu, 512 / ((attr.numRegs + 7) / 8 * 8));
-  return std::max(per_cu, 1);
+  // the hardware limit of a (kernel, LDS size) pair, asked once: the two
+  // runtime queries cost host time on every launch of a small call
+  static std::mutex mu;
+  static std::map<std::pair<const void*, size_t>, int> limit;
+  int hw = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = limit.find({kernel, lds_bytes});
+    if (it != limit.end()) hw = it->second;
+  }
+  if (hw == 0) {
+    hw = 64;
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kernel, kThreadsPerBlock, lds_bytes) ==
+            hipSuccess &&
+        b > 0)
+      hw = std::min(hw, b);
+    hipFuncAttributes attr{};
+    if (hipFuncGetAttributes(&attr, kernel) == hipSuccess && attr.numRegs > 0)
+      hw = std::min(hw, 512 / ((attr.numRegs + 7) / 8 * 8));
+    std::lock_guard<std::mutex> lk(mu);
+    limit[{kernel, lds_bytes}] = hw;
+  }
+  return std::max(std::min(max_per_cu, hw), 1);
+}
+
+// Compute units of the current device (asked once per device).
+inline int device_cus() {
+  static std::atomic<int> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  int cus = cache[dev].load(std::memory_order_relaxed);
+  if (cus == 0) {
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+    cache[dev].store(cus, std::memory_order_relaxed);
+  }
+  return cus;
 }
 
 inline int grid_for(const void* kernel, size_t lds_bytes, uint32_t items, int max_per_cu) {
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const uint32_t resident = static_cast<uint32_t>(cus * resident_per_cu(kernel, lds_bytes, max_per_cu));
+  const uint32_t resident =
+      static_cast<uint32_t>(device_cus() * resident_per_cu(kernel, lds_bytes, max_per_cu));
   return static_cast<int>(items < resident ? (items ? items : 1) : resident);
 }
 
@@ -1432,9 +1462,7 @@ hipError_t launch_edges_apart(Kern kern, Params p, size_t lds, uint32_t interior
                               int* grid_out = nullptr) {
   p.edge_blocks = 0;
   const void* k = reinterpret_cast<const void*>(kern);
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int cus = device_cus();
   const uint32_t e = (std::min<uint32_t>(edge_items, static_cast<uint32_t>(cus)) + 7u) & ~7u;
   if (!env_flag("ECAMD_EDGE_BLOCKS", kEdgeBlocks) || edge_items == 0 || interior_items == 0 ||
       !lds_starts_at_zero(k))
