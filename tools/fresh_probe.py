@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Where a decode with new erasure masks spends its time (dev tool): the host
 call (enqueue) time and the GPU event span, for masks drawn anew per call
-against the same masks repeated, at bench.py's workload (k=10 m=4,
-256 x 4 MiB)."""
+(new patterns: decode rows and table sets built on the host), masks
+reshuffled per call from 50 patterns already in the device pool (new
+descriptors only), and the same masks repeated (cached descriptors), at
+bench.py's workload (k=10 m=4, 256 x 4 MiB)."""
 import os
 import sys
 import time
@@ -31,10 +33,18 @@ def main():
         return [full & ~int(sum(1 << int(i) for i in rng.choice(k + m, 4, replace=False)))
                 for _ in range(B)]
 
-    for label, seeds in (("fresh", range(100, 112)), ("repeat", [7] * 12)):
+    pool = masks(3)[:50]  # 50 patterns, cached in the device pool after the first call
+
+    def shuffled(seed):
+        rng = np.random.default_rng(seed)
+        return [pool[int(i)] for i in rng.integers(0, len(pool), B)]
+
+    for label, seeds, gen in (("fresh", range(100, 112), masks),
+                              ("reshuffled", range(200, 212), shuffled),
+                              ("repeat", [7] * 12, masks)):
         host_us, span_us = [], []
         for s in seeds:
-            mk = masks(s)
+            mk = gen(s)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0 = time.perf_counter()
