@@ -909,7 +909,10 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
   }
 
   // cache key: everything the descriptor bytes depend on besides the pool
-  std::vector<uint8_t> key;
+  // (this thread's buffers are reused from call to call: the per-object
+  // vectors of a 256-object batch were 256+ allocations per call)
+  thread_local std::vector<uint8_t> key;
+  key.clear();
   key_append(key, J.masks, J.n_obj);
   if (J.dest) key_append(key, J.dest, J.n_obj);
   if (J.headers) key_append(key, J.headers, static_cast<size_t>(J.n_obj) * kHeaderBytes);
@@ -925,10 +928,10 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
     return e2 == hipSuccess ? 0 : hip_errno(e2);
   }
 
-  DescBatch B;
+  thread_local DescBatch B;
   B.base.resize(J.n_obj);
   B.slots.resize(J.n_obj);
-  B.outs.resize(J.n_obj);
+  if (B.outs.size() < static_cast<size_t>(J.n_obj)) B.outs.resize(J.n_obj);
   int o0 = 0;  // first object not yet launched
   bool split = false;
   for (int o = 0; o < J.n_obj; ++o) {
