@@ -101,6 +101,14 @@ def parse(argv=None):
                     help="decode steps whose erasure masks are new every step (drawn from "
                          "the seed outside the clock, handed over inside it): timed apart "
                          "from the headline step, which replays one batch of masks")
+    ap.add_argument("--full-stripe-steps", type=int, default=10,
+                    help="launches of the full-stripe encode (k data + m parity fragments, "
+                         "headers included: liberasurecode_encode's output) timed after the "
+                         "headline steps; 0 = skip")
+    ap.add_argument("--swift-procs", default="1,4,15",
+                    help="process counts of the Swift call-shape leg (tools/swift_calls.py: "
+                         "P processes calling ECDriver.encode / decode per segment); '' = skip")
+    ap.add_argument("--swift-seconds", type=float, default=1.0)
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0 (exercises the N-rank path on one GPU)")
     ap.add_argument("--no-numa", action="store_true",
@@ -251,28 +259,36 @@ def oracle_pass(args, host, masks, dests, gpu_frags=None, gpu_second=None, sampl
     return t_enc, t_two, bad, oc.src
 
 
-def _cpu_worker(path, shape, lo, hi, args_dict, masks, dests, barrier, q):
+def _cpu_worker(path, shape, lo, hi, args_dict, masks, dests, barrier, q, repeat=1):
     """One CPU-baseline process: encode + decode/reconstruct objects [lo, hi)
-    with the scalar oracle, after every worker is ready."""
+    with the scalar oracle, `repeat` times, after every worker is ready (one
+    untimed warm-up pass over its first object: tables built, pages in)."""
     host = np.memmap(path, dtype=np.uint8, mode="r", shape=shape)
     a = argparse.Namespace(**args_dict)
     oc = OracleCodec(a.ec_type, a.k, a.m, a.obj_bytes, crc=getattr(a, "inline_crc32", False))
     np.asarray(host[lo:hi]).sum()  # page the slice in before the clock starts
-    barrier.wait()
-    t0 = time.perf_counter()
-    for o in range(lo, hi):
+
+    def one(o):
         oc.encode(host[o, :a.obj_bytes])
         if a.second == "decode":
             oc.decode(masks[o])
         else:
             oc.reconstruct(masks[o], dests[o])
+    if hi > lo:
+        one(lo)
+    barrier.wait()
+    t0 = time.perf_counter()
+    for _ in range(repeat):
+        for o in range(lo, hi):
+            one(o)
     q.put(time.perf_counter() - t0)
 
 
-def cpu_parallel(args, host, masks, dests, sample, workers):
+def cpu_parallel(args, host, masks, dests, sample, workers, repeat=1):
     """The oracle over objects [0, sample) in `workers` spawned processes
     (fresh interpreters that never touch the GPU; objects shared through a
-    memory-mapped temporary file).  Returns the seconds of the slowest worker."""
+    memory-mapped temporary file), each worker's share `repeat` times.
+    Returns the seconds of the slowest worker."""
     import multiprocessing as mp
     import tempfile
     shape = (sample, host.shape[1])
@@ -291,7 +307,7 @@ def cpu_parallel(args, host, masks, dests, sample, workers):
         for w in range(workers):
             lo, hi = sample * w // workers, sample * (w + 1) // workers
             p = ctx.Process(target=_cpu_worker,
-                            args=(path, shape, lo, hi, ad, masks, dests, barrier, q))
+                            args=(path, shape, lo, hi, ad, masks, dests, barrier, q, repeat))
             p.start()
             procs.append(p)
         times = []
@@ -384,19 +400,22 @@ def host_resident(args, codec, host, stripes, masks, fs, bs, reps=3):
                      ("staged_out", {"ECAMD_HOST_STAGED": "1", "ECAMD_HOST_STAGED_OUT": "1"})):
         os.environ.update(env)
         try:
+            # the knobs are read when an instance is created
+            from pyeclib_amd import batch
+            c2 = batch.BatchCodec(k, m, ec_type=args.ec_type, inline_crc32=args.inline_crc32)
             hpar2 = torch.zeros_like(hpar).pin_memory()
-            codec.encode_host(pinned, n, hpar2)
+            c2.encode_host(pinned, n, hpar2)
             t0 = time.perf_counter()
             for _ in range(reps):
-                codec.encode_host(pinned, n, hpar2)
+                c2.encode_host(pinned, n, hpar2)
             out[f"host_{tag}_encode_GiBps"] = round(B * n / ((time.perf_counter() - t0) / reps) / 2**30, 3)
             ok = ok and torch.equal(hpar2[:, :, :80 + bs], hpar[:, :, :80 + bs])
             if args.second == "decode":
                 hout.zero_()
-                codec.decode_host(hfr, n, masks, hout)
+                c2.decode_host(hfr, n, masks, hout)
                 t0 = time.perf_counter()
                 for _ in range(reps):
-                    codec.decode_host(hfr, n, masks, hout)
+                    c2.decode_host(hfr, n, masks, hout)
                 out[f"host_{tag}_decode_GiBps"] = round(B * n / ((time.perf_counter() - t0) / reps) / 2**30, 3)
                 ok = ok and torch.equal(hout[:, :n], pinned[:, :n])
         finally:
@@ -563,6 +582,45 @@ def config0_cli(args, size=1 << 20, reps=5):
 
 # ---------------- decode with erasures that change every step ----------------
 
+def fresh_decode_steady(args, codec, stripes, objs, out, stream, B, rank):
+    """Decode with erasures drawn anew for every call, back to back: the
+    masks of all `--fresh-steps` calls are drawn first (outside the clock),
+    then the calls are made with no synchronisation between them, so call
+    i+1's host work (first-k choice, decode rows and tables of new patterns,
+    descriptors and their copy -- what the reference redoes in every decode,
+    pyeclib_c.c:878) overlaps call i's kernel, as a server streaming decodes
+    would run.  Reported per call: GPU event span / calls, and host wall /
+    calls.  Every call decodes the same objects, so the last call's output is
+    compared with them; each call's output is also checked, against the
+    objects, by the idle-GPU variant (fresh_decode)."""
+    import torch
+    k, m, n = args.k, args.m, args.obj_bytes
+    steps = max(2, args.fresh_steps)
+    all_masks = []
+    for i in range(steps):
+        rng = np.random.Generator(np.random.PCG64(SEED + rank + 7919 * (i + 1)))
+        all_masks.append(erasure_masks(rng, B, k, m, args.erasures))
+    out.zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for masks in all_masks:
+        codec.decode(stripes, n, masks, out)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ok = bool(torch.equal(out[:, :n], objs[:, :n]))
+    return {"decode_fresh_ms": round(e0.elapsed_time(e1) / steps, 4),
+            "decode_fresh_wall_ms": round(1e3 * wall / steps, 4),
+            "decode_fresh_steps": steps,
+            "decode_fresh_note": "steady state: new erasure masks for every call (PCG64 seed + "
+                                 "rank + 7919*call, drawn before the clock), calls back to back "
+                                 "with no sync between them, so each call's host descriptor/table "
+                                 "build and H2D overlap the previous call's kernel; per call = "
+                                 "event span / calls; last output compared with the objects"}, ok
+
+
 def fresh_decode(args, codec, stripes, objs, out, stream, B, rank):
     """`--fresh-steps` decode steps whose masks are drawn anew each step (seed
     + rank + step, outside the clock) and handed to the call inside it, so
@@ -589,13 +647,13 @@ def fresh_decode(args, codec, stripes, objs, out, stream, B, rank):
         wall_ms.append(1e3 * (time.perf_counter() - t0))
         gpu_ms.append(ev[i][0].elapsed_time(ev[i][1]))
         ok = ok and bool(torch.equal(out[:, :n], objs[:, :n]))
-    return {"decode_fresh_ms": round(float(np.mean(gpu_ms)), 4),
-            "decode_fresh_first_ms": round(gpu_ms[0], 4),
-            "decode_fresh_wall_ms": round(float(np.mean(wall_ms)), 4),
-            "decode_fresh_steps": args.fresh_steps,
-            "decode_fresh_note": "new erasure masks every step (PCG64 seed + rank + 1000*step); "
-                                 "event span from an idle GPU, host descriptor build + H2D + "
-                                 "kernel; every step's objects compared with the originals"}, ok
+    return {"decode_fresh_idle_ms": round(float(np.mean(gpu_ms)), 4),
+            "decode_fresh_idle_first_ms": round(gpu_ms[0], 4),
+            "decode_fresh_idle_wall_ms": round(float(np.mean(wall_ms)), 4),
+            "decode_fresh_idle_note": "new erasure masks every step (PCG64 seed + rank + "
+                                      "1000*step), each from an idle GPU (sync before): event "
+                                      "span = host descriptor build + H2D + kernel + clock ramp; "
+                                      "every step's objects compared with the originals"}, ok
 
 
 def main():
@@ -792,9 +850,38 @@ def main():
     if two == "decode" and args.fresh_steps > 0:
         fresh, fresh_ok = fresh_decode(args, codec, stripes, objs, out, stream, B, rank)
         result.update(fresh)
+        steady, steady_ok = fresh_decode_steady(args, codec, stripes, objs, out, stream, B, rank)
+        result.update(steady)
+        fresh_ok = fresh_ok and steady_ok
         # the headline batch is decoded again so the oracle check below sees it
         codec.decode(stripes, n, masks, out)
         torch.cuda.synchronize()
+
+    # ---- full-stripe encode: liberasurecode_encode's whole output (k data +
+    # m parity fragments, headers included) in one launch per batch; the
+    # verification below then checks the stripes this leg wrote ----
+    if args.full_stripe_steps > 0:
+        ev_fs = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        par_ref = p_parity.clone()  # the headline (parity-only) encode's output
+        stripes[:, :k].zero_()
+        codec.encode(objs, n, parity=p_parity, data=stripes[:, :k])
+        torch.cuda.synchronize()
+        ev_fs[0].record(stream)
+        for _ in range(args.full_stripe_steps):
+            codec.encode(objs, n, parity=p_parity, data=stripes[:, :k])
+        ev_fs[1].record(stream)
+        torch.cuda.synchronize()
+        fs_ms = ev_fs[0].elapsed_time(ev_fs[1]) / args.full_stripe_steps
+        parity_same = bool(torch.equal(p_parity, par_ref))
+        del par_ref
+        fs_bytes = B * n + B * (k + m) * (bs + 80)
+        result["encode_full_stripe_ms"] = round(fs_ms, 4)
+        result["encode_full_stripe"] = {
+            "bytes": fs_bytes, "GBps": round(fs_bytes / (fs_ms * 1e-3) / 1e9, 1),
+            "frac": round(fs_bytes / (fs_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "launches": args.full_stripe_steps,
+            "note": "k data + m parity fragments with headers per object in one launch, back "
+                    "to back; these stripes are the ones the oracle check below compares"}
 
     # ---- verification of the timed batch (every object), and the CPU baseline ----
     bad = []
@@ -808,6 +895,8 @@ def main():
         del gpu_frags, gpu_second
     if not fresh_ok:
         bad.append((-1, "fresh-erasure decode"))
+    if args.full_stripe_steps > 0 and not parity_same:
+        bad.append((-1, "headline parity differs from the full-stripe encode's"))
     verified = bool(shard.min_over_ranks(0 if bad else 1)) and not args.no_verify
     result["verified"] = verified
     if not args.no_verify:
@@ -825,28 +914,56 @@ def main():
         result.update(single_object_calls(args))
     if rank == 0 and args.config0:
         result.update(config0_cli(args))
+    if rank == 0 and world == 1 and args.swift_procs and not args.no_host and w == 16:
+        # the Swift call shape: P processes, one ECDriver call per segment
+        # (this process holds the GPU too: at most 15 workers beside it)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import swift_calls
+        procs = tuple(min(15, int(x)) for x in args.swift_procs.split(",") if x)
+        rows = swift_calls.sweep(procs, (1 << 20, 4 << 20), args.swift_seconds)
+        result["swift_calls"] = {
+            f"{r['op']}_{r['size'] >> 20}MiB_P{r['procs']}":
+                {"GiBps": r["GiBps"], "us_per_call": r["us_per_call_median"]} for r in rows}
+        result["swift_calls_verified"] = all(r["verified"] for r in rows)
+        result["swift_calls_note"] = (
+            "P worker processes on this GPU, each its own ECDriver(10, 4, liberasurecode_rs_vand) "
+            "calling encode (or decode, 4 data fragments missing) on its own pageable segment "
+            f"back to back for {args.swift_seconds} s; aggregate segment GiB/s over the span from "
+            "the first start to the last finish; us_per_call = median over processes")
 
     if rank == 0 and not args.no_cpu_baseline and (world == 1 or args.cpu_baseline_all):
         sample = min(args.cpu_sample or B, B)
         if t_enc is None or sample != B:
             t_enc, t_two, _, src = oracle_pass(args, host, two_masks, dests, sample=sample)
+        # N = every CPU this process may run on (the whole
+        # node's share after the NUMA binding), the objects split evenly;
+        # the 16-worker figure (the box's CPU share per GPU) beside it
         affinity = len(os.sched_getaffinity(0))
-        workers = max(1, min(affinity, CPU_WORKERS_PER_GPU * world, sample))
-        t_par = cpu_parallel(args, host, two_masks, dests, sample, workers)
+        workers = max(1, min(affinity, sample))
+        # each worker's share repeated to >= 16 object passes (~0.2 s at 4 MiB),
+        # so start-up jitter across many processes does not set the time
+        rep = max(1, -(-16 * workers // sample))
+        t_par = cpu_parallel(args, host, two_masks, dests, sample, workers, rep)
+        w16 = max(1, min(affinity, CPU_WORKERS_PER_GPU * world, sample))
+        rep16 = max(1, -(-16 * w16 // sample))
+        t_16 = cpu_parallel(args, host, two_masks, dests, sample, w16, rep16)
         one = 2 * sample * n / (t_enc + t_two) / 2**30
         result["cpu_baseline"] = {
-            "value": round(2 * sample * n / t_par / 2**30, 4),
+            "value": round(2 * sample * n * rep / t_par / 2**30, 4),
             "unit": "GiB/s", "cores": workers, "kind": "port",
             "sample": f"{sample} objects x {n} B: encode + {two} ({src}, {args.ec_type}), "
-                      f"{workers} single-threaded worker processes (objects split evenly)",
+                      f"{workers} single-threaded worker processes = every CPU of the "
+                      f"process's affinity (objects split evenly, each share {rep}x)",
             "cpu_model": cpu_model(),
             "affinity_cpus": affinity,
             "numa_node": numa_all.get("numa_node"),
+            "value_16_workers": round(2 * sample * n * rep16 / t_16 / 2**30, 4),
             "single_core_value": round(one, 4),
             "single_core_encode_GiBps": round(sample * n / t_enc / 2**30, 4),
             f"single_core_{two}_GiBps": round(sample * n / t_two / 2**30, 4),
             "single_core_seconds": round(t_enc + t_two, 2),
             "parallel_seconds": round(t_par, 3),
+            "parallel_seconds_16_workers": round(t_16, 3),
         }
     if rank == 0:
         print(json.dumps(result), flush=True)

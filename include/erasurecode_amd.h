@@ -161,6 +161,28 @@ uint32_t liberasurecode_get_version(void);
 /* Payload bytes per fragment for objects of obj_len bytes. */
 uint64_t ecamd_blocksize(int desc, uint64_t obj_len);
 
+/* liberasurecode_encode (pyeclib_c.c:537) into caller-allocated fragments:
+ * the same k + m fragments (80-byte header + payload each), written into
+ * fragments[0 .. k+m-1], each fragment_len = blocksize + 80 bytes (else
+ * -EINVALIDPARAMS).  A binding that owns its output objects (pyeclib_c wraps
+ * liberasurecode's buffers in new bytes objects, pyeclib_c.c:544-560) can
+ * hand their storage here and skip that copy.  Synchronous; 0 or -errno. */
+int ecamd_encode_into(int desc, const char *data, uint64_t data_len, char **fragments,
+                      uint64_t fragment_len);
+
+/* Host-side phases of the instance's last single-object encode / decode,
+ * in microseconds: [0] staging copy in, [1] launch, [2] host work beside the
+ * kernel (encode: the data fragments), [3] wait for the kernel, [4] copy
+ * out, [5] headers.  Returns the count written (<= n) or -errno. */
+int ecamd_call_phases(int desc, double *us, int n);
+
+/* liberasurecode_decode (pyeclib_c.c:878) into a caller buffer of exactly
+ * the decoded length (orig_data_size of the fragments' headers; else
+ * -EINVALIDPARAMS).  Same checks, fast path and errors; synchronous. */
+int ecamd_decode_into(int desc, char **available_fragments, int num_fragments,
+                      uint64_t fragment_len, int force_metadata_checks, char *out,
+                      uint64_t out_len);
+
 /* Encode n_obj objects of obj_len bytes resident in HBM.
  *   d_objs:   object o at d_objs + o*obj_stride (obj_stride % 16 == 0)
  *   d_parity: parity fragment p of object o (80-byte header + payload) at
@@ -171,7 +193,13 @@ uint64_t ecamd_blocksize(int desc, uint64_t obj_len);
  *   stripe_stride % 16 == 0.  A full-stripe layout [n_obj][k+m][frag_stride]
  *   is d_data = base, d_parity = base + k*frag_stride,
  *   stripe_stride = (k+m)*frag_stride.
- * Asynchronous on `stream`; returns 0 or -errno. */
+ * Asynchronous on `stream`; returns 0 or -errno.
+ * Streams: an instance orders the rewrite of its own device buffers (cached
+ * descriptors, decode table pool) after its earlier launches on every stream
+ * it was given, with GPU-side event waits -- never a device-wide
+ * synchronisation -- so a stream passed to any ecamd_* call must remain valid
+ * until the instance is destroyed (liberasurecode_instance_destroy waits for
+ * the instance's work on those streams). */
 int ecamd_encode_batch(int desc, const void *d_objs, uint64_t obj_stride, uint64_t obj_len,
                        int n_obj, void *d_parity, void *d_data, uint64_t frag_stride,
                        uint64_t stripe_stride, void *stream);

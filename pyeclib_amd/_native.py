@@ -22,6 +22,11 @@ from . import exceptions as _local_exc
 
 _LIB_NAME = "libpyeclib_amd.so"
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), _LIB_NAME)
+# Developer A/B runs only (tools/ab_bench.py): load another build of the
+# same C ABI, e.g. tools/build/libpyeclib_amd_ab.so (`make -C
+# pyeclib_amd/csrc ab`).  The product library has no switches of its own.
+if os.environ.get("PYECLIB_AMD_LIBRARY"):
+    _LIB_PATH = os.path.abspath(os.environ["PYECLIB_AMD_LIBRARY"])
 
 if not os.path.exists(_LIB_PATH):
     raise ImportError(
@@ -172,6 +177,13 @@ _sig = {
                                                     _P(ctypes.c_int), ctypes.c_void_p,
                                                     ctypes.c_uint64]),
 }
+_sig.update({
+    "ecamd_encode_into": (ctypes.c_int, [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                         _P(ctypes.c_void_p), ctypes.c_uint64]),
+    "ecamd_decode_into": (ctypes.c_int, [ctypes.c_int, _cpp, ctypes.c_int, ctypes.c_uint64,
+                                         ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64]),
+    "ecamd_call_phases": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_double), ctypes.c_int]),
+})
 EXPORTS = tuple(_sig)
 for _name, (_res, _args) in _sig.items():
     _fn = getattr(lib, _name)
@@ -252,6 +264,21 @@ def _frag_array(frags: Sequence[bytes]) -> ctypes.Array:
     return (ctypes.c_char_p * len(frags))(*frags)
 
 
+# New bytes objects whose storage the library fills (the C-API pattern
+# PyBytes_FromStringAndSize(NULL, n), then write, then share): pyeclib_c
+# copies liberasurecode's fragment buffers into new bytes objects
+# (Py_BuildValue("y#"), pyeclib_c.c:544-560); here the library writes the
+# fragments (or the decoded object) into the bytes objects' own storage, and
+# that whole-object copy is gone.  Only ever called with n >= 1, and the
+# objects are not shared before they are filled.
+_new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.restype = ctypes.py_object
+_new_bytes.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+_bytes_ptr = ctypes.pythonapi.PyBytes_AsString
+_bytes_ptr.restype = ctypes.c_void_p
+_bytes_ptr.argtypes = [ctypes.py_object]
+
+
 # ---- the eleven module functions ----
 
 def init(k: int, m: int, backend_id: int, hd: int = 0, use_inline_chksum: int = 0,
@@ -288,19 +315,14 @@ def encode(handle: PyECLibHandle, data: Any) -> list[bytes]:
         buf, n = _as_buffer(data)
     except TypeError:
         raise_error(-EINVALIDPARAMS, fn)
-    dat = _P(ctypes.c_void_p)()
-    par = _P(ctypes.c_void_p)()
-    flen = ctypes.c_uint64(0)
-    ret = lib.liberasurecode_encode(h.desc, buf, n, ctypes.byref(dat), ctypes.byref(par),
-                                    ctypes.byref(flen))
+    # liberasurecode_encode's fragments, written straight into the bytes
+    # objects returned (ecamd_encode_into: same bytes, no copy out)
+    fl = int(lib.ecamd_blocksize(h.desc, n)) + HEADER_SIZE
+    out = [_new_bytes(None, fl) for _ in range(h.k + h.m)]
+    ptrs = (ctypes.c_void_p * len(out))(*[_bytes_ptr(b) for b in out])
+    ret = lib.ecamd_encode_into(h.desc, buf, n, ptrs, fl)
     if ret < 0:
         raise_error(ret, fn)
-    try:
-        fl = flen.value
-        out = [ctypes.string_at(dat[i], fl) for i in range(h.k)]
-        out += [ctypes.string_at(par[i], fl) for i in range(h.m)]
-    finally:
-        lib.liberasurecode_encode_cleanup(h.desc, dat, par)
     return out
 
 
@@ -325,6 +347,24 @@ def decode(handle: PyECLibHandle, fragments: list[bytes], fragment_len: int,
         arr = _frag_array(fragments)
     except TypeError:
         raise_error(-EINVALIDPARAMS, fn)
+    fl = int(fragment_len)
+    n_out = _decoded_len(fragments, fl, h.k)
+    if n_out is not None:
+        # into a new bytes object of the decoded length (ecamd_decode_into)
+        res = _new_bytes(None, n_out) if n_out else b""
+        ret = lib.ecamd_decode_into(h.desc, arr, len(fragments), fl,
+                                    1 if force_metadata_checks else 0,
+                                    _bytes_ptr(res) if n_out else None, n_out)
+        if ret < 0:
+            raise_error(ret, fn)
+        if not spans:
+            return res
+        pieces = []
+        for off, length in spans:
+            if off < 0 or length < 0 or off + length > n_out:
+                raise_error(-EINVALIDPARAMS, "pyeclib_c_decode invalid range")
+            pieces.append(res[off:off + length])
+        return pieces
     out = ctypes.c_void_p()
     olen = ctypes.c_uint64(0)
     ret = lib.liberasurecode_decode(h.desc, arr, len(fragments), int(fragment_len),
@@ -344,6 +384,17 @@ def decode(handle: PyECLibHandle, fragments: list[bytes], fragment_len: int,
         return pieces
     finally:
         lib.liberasurecode_decode_cleanup(h.desc, out)
+
+
+def _decoded_len(fragments: list[bytes], fragment_len: int, k: int) -> int | None:
+    """orig_data_size from the first fragment's header when it is plausible
+    (the payload sizes of k fragments hold it); None sends the call through
+    liberasurecode_decode, whose checks produce the error a bad header deserves."""
+    f = fragments[0]
+    if not isinstance(f, bytes) or len(f) < HEADER_SIZE or fragment_len < HEADER_SIZE:
+        return None
+    n = int.from_bytes(f[12:20], "little")
+    return n if n <= k * (fragment_len - HEADER_SIZE) else None
 
 
 def reconstruct(handle: PyECLibHandle, fragments: list[bytes], fragment_len: int,

@@ -1,6 +1,12 @@
 // Field / k dispatch of the region kernels (ec_kernels.hpp, ec_inst.hpp).
 #include "ec_kernels.hpp"
 
+#ifdef ECAMD_AB
+#include <map>
+#include <mutex>
+#include <string>
+#endif
+
 namespace ecamd {
 
 hipError_t launch_enc16_1(const EncodeParams&, hipStream_t); hipError_t launch_enc16_2(const EncodeParams&, hipStream_t); hipError_t launch_enc16_3(const EncodeParams&, hipStream_t); hipError_t launch_enc16_4(const EncodeParams&, hipStream_t); hipError_t launch_enc16_5(const EncodeParams&, hipStream_t); hipError_t launch_enc16_6(const EncodeParams&, hipStream_t); hipError_t launch_enc16_7(const EncodeParams&, hipStream_t); hipError_t launch_enc16_8(const EncodeParams&, hipStream_t); hipError_t launch_enc16_9(const EncodeParams&, hipStream_t); hipError_t launch_enc16_10(const EncodeParams&, hipStream_t); hipError_t launch_enc16_11(const EncodeParams&, hipStream_t); hipError_t launch_enc16_12(const EncodeParams&, hipStream_t); hipError_t launch_enc16_13(const EncodeParams&, hipStream_t); hipError_t launch_enc16_14(const EncodeParams&, hipStream_t); hipError_t launch_enc16_15(const EncodeParams&, hipStream_t); hipError_t launch_enc16_16(const EncodeParams&, hipStream_t); hipError_t launch_enc16_17(const EncodeParams&, hipStream_t); hipError_t launch_enc16_18(const EncodeParams&, hipStream_t); hipError_t launch_enc16_19(const EncodeParams&, hipStream_t); hipError_t launch_enc16_20(const EncodeParams&, hipStream_t); hipError_t launch_enc16_21(const EncodeParams&, hipStream_t); hipError_t launch_enc16_22(const EncodeParams&, hipStream_t); hipError_t launch_enc16_23(const EncodeParams&, hipStream_t); hipError_t launch_enc16_24(const EncodeParams&, hipStream_t); hipError_t launch_enc16_25(const EncodeParams&, hipStream_t); hipError_t launch_enc16_26(const EncodeParams&, hipStream_t); hipError_t launch_enc16_27(const EncodeParams&, hipStream_t); hipError_t launch_enc16_28(const EncodeParams&, hipStream_t); hipError_t launch_enc16_29(const EncodeParams&, hipStream_t); hipError_t launch_enc16_30(const EncodeParams&, hipStream_t); hipError_t launch_enc16_31(const EncodeParams&, hipStream_t);
@@ -164,4 +170,31 @@ hipError_t launch_decode(const DecodeParams& p, hipStream_t stream) {
   return p.w == 8 ? dispatch_dec8(p, stream) : dispatch_dec16(p, stream);
 }
 
+#ifdef ECAMD_AB
+// A/B builds: the launchers' switches, set by name from the A/B tools
+// (ecamd_ab_set); unset names read their default.
+namespace {
+std::mutex g_ab_mu;
+std::map<std::string, int> g_ab;
+}  // namespace
+
+int ab_knob(const char* name, int dflt) {
+  std::lock_guard<std::mutex> lk(g_ab_mu);
+  auto it = g_ab.find(name);
+  return it == g_ab.end() ? dflt : it->second;
+}
+#endif
+
 }  // namespace ecamd
+
+#ifdef ECAMD_AB
+// Set (value >= 0) or clear (value < 0) an A/B switch; returns 0.
+extern "C" int ecamd_ab_set(const char* name, int value) {
+  std::lock_guard<std::mutex> lk(ecamd::g_ab_mu);
+  if (value < 0)
+    ecamd::g_ab.erase(name);
+  else
+    ecamd::g_ab[name] = value;
+  return 0;
+}
+#endif

@@ -12,7 +12,8 @@
 namespace ecamd {
 
 // GF(2^16) encode: <= 2 rows per pass need only the low dword of each table
-// entry (Gf16<1>).
+// entry (Gf16<1>); 5..8 rows run in one eight-row pass (Gf16x8, its rows
+// past p.nrows dropped).
 #define ECAMD_ENC16(K)                                                      \
   hipError_t launch_enc16_##K(const EncodeParams& p, hipStream_t s) {       \
     switch (p.nrows) {                                                      \
@@ -20,6 +21,8 @@ namespace ecamd {
       case 2: return launch_encode_k<Gf16<1>, K, 2>(p, s);                  \
       case 3: return launch_encode_k<Gf16<2>, K, 3>(p, s);                  \
       case 4: return launch_encode_k<Gf16<2>, K, 4>(p, s);                  \
+      case 5: case 6: case 7: case 8:                                       \
+        return launch_encode_k<Gf16x8, K, 8>(p, s);                         \
       default: return hipErrorInvalidValue;                                 \
     }                                                                       \
   }

@@ -39,12 +39,20 @@ __host__ __device__ constexpr uint32_t table_slot_bytes(uint32_t k, uint32_t w) 
   return (k * table_bytes_per_input(w) + 255u) & ~255u;
 }
 
-// ECAMD_XCD=0 turns off the XCD-major work split (every kernel).
-// ECAMD_EDGE_SIDE=1 runs the edge items in a launch of their own on a side
-// stream (the round-2 variant, for A/B runs) instead of in the interior launch.
-// ECAMD_ENC_NOCOMP=1 / ECAMD_DEC_NOCOMP=1: memory-only probes of the
-// benchmark case (k = 10; wrong output), read at each launch so
-// tools/ab_bench.py can time them beside the real kernels in one process.
+// A/B builds.  The product library has no tuning switches: every launch
+// takes the measured default, and nothing is read from the environment on
+// the launch path.  `make -C pyeclib_amd/csrc ab` builds a separate library
+// (tools/build/libpyeclib_amd_ab.so, -DECAMD_AB) in which the launchers also
+// instantiate the alternative kernels of past A/B runs -- including the
+// memory-only probes ECAMD_ENC_NOCOMP / ECAMD_DEC_NOCOMP, whose output is
+// WRONG -- selected by name through ecamd_ab_set() (tools/ab_bench.py).
+#ifdef ECAMD_AB
+constexpr bool kAB = true;
+int ab_knob(const char* name, int dflt);  // ec_dispatch.cpp
+#else
+constexpr bool kAB = false;
+inline int ab_knob(const char*, int dflt) { return dflt; }
+#endif
 
 struct EncodeParams {
   const uint8_t* objs;      // object o at objs + o * obj_stride
@@ -67,6 +75,8 @@ struct EncodeParams {
   uint32_t fused_edges;        // set by the launcher: edge items run in the interior launch
   uint32_t edge_blocks;        // set by the launcher: blocks [0, edge_blocks) run only the edge
                                // items; 0 = every block runs its share of them first
+  uint32_t no_edge_blocks;     // caller: 1 = never run the edge items in blocks of their own
+                               // (the round-2 launch form; instance knob ECAMD_EDGE_BLOCKS=0)
   // inline_crc32 fused into the encode (null: no parity CRC in this launch):
   // CrcTables (its raw16 / z4096 / level maps), CrcFinishTables for
   // (bs, ceil(bs / 4096)), and n_obj * ceil(bs / 4096) * m u32 of run
@@ -113,6 +123,7 @@ struct DecodeParams {
   uint32_t xcd_split;          // set by the launcher (item_range)
   uint32_t fused_edges;        // set by the launcher: edge items run in the interior launch
   uint32_t edge_blocks;        // set by the launcher (see EncodeParams)
+  uint32_t no_edge_blocks;     // caller (see EncodeParams)
 };
 
 // Dispatch on (p.w, p.k) to the per-k instantiations (ec_dispatch.cpp).

@@ -45,6 +45,7 @@
 #include <atomic>
 #include <map>
 #include <mutex>
+#include <tuple>
 #include <utility>
 #include <unordered_map>
 
@@ -311,6 +312,69 @@ struct Gf16 {
     return __builtin_amdgcn_perm(b, a, (r & 1) ? 0x07060302u : 0x05040100u);
   }
   // Output row r of the 8 accumulated symbols as a 16-byte chunk.
+  static __device__ __forceinline__ uint4 row(const Acc& a, int r) {
+    return make_uint4(pack(a.s[0], a.s[1], r), pack(a.s[2], a.s[3], r), pack(a.s[4], a.s[5], r),
+                      pack(a.s[6], a.s[7], r));
+  }
+};
+
+// Eight output rows per lookup (encode with 4 < m <= 8 in one pass: the
+// object is read once instead of once per four rows).  Entry (c, q, v) is a
+// u128 holding the products of rows 0..7 (gf16.hpp build_nibble_tables_x8),
+// at byte 1024c + 256q + 16v: one ds_read_b128 per nibble.  A 16-entry table
+// spans all 64 banks in 16-B entries, so any 16 lanes of a ds_read_b128 lane
+// group read it conflict-free.  Tables at LDS 0 only (encode).
+__device__ __forceinline__ v4u lds_u128(uint32_t a, uint32_t tab) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) v4u*>(
+      reinterpret_cast<const lds_char*>(static_cast<uintptr_t>(a)) + tab);
+}
+struct Gf16x8 {
+  static constexpr uint32_t kW = 16;
+  static constexpr int kRows = 8;
+  static constexpr uint32_t kTableBytes = 1024;
+  struct Acc {
+    v4u s[8];  // s[2d] / s[2d+1]: rows 0-7 of the low / high symbol of input dword d
+  };
+  static __device__ __forceinline__ uint32_t kb(uint32_t base) { return base >> 8; }
+  static __device__ __forceinline__ void zero(Acc& a) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a.s[i] = v4u{0u, 0u, 0u, 0u};
+  }
+  static __device__ __forceinline__ void pin(Acc& a) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      asm volatile("" : "+v"(a.s[i].x), "+v"(a.s[i].y), "+v"(a.s[i].z), "+v"(a.s[i].w));
+  }
+  static constexpr uint32_t qoff(int q) { return 256u * q; }
+  static __device__ __forceinline__ void mac_dword(uint32_t tab, uint32_t x, v4u& s_lo, v4u& s_hi) {
+    uint32_t a[8];
+    Gf16<2>::addrs<true>(0, x, a);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      v4u& s = h ? s_hi : s_lo;
+      const v4u e0 = lds_u128(a[4 * h], tab + qoff(0)), e1 = lds_u128(a[4 * h + 1], tab + qoff(1)),
+                e2 = lds_u128(a[4 * h + 2], tab + qoff(2)), e3 = lds_u128(a[4 * h + 3], tab + qoff(3));
+      s.x = xor3(xor3(s.x, e0.x, e1.x), e2.x, e3.x);
+      s.y = xor3(xor3(s.y, e0.y, e1.y), e2.y, e3.y);
+      s.z = xor3(xor3(s.z, e0.z, e1.z), e2.z, e3.z);
+      s.w = xor3(xor3(s.w, e0.w, e1.w), e2.w, e3.w);
+      asm volatile("" : "+v"(s.x), "+v"(s.y), "+v"(s.z), "+v"(s.w));
+      lookup_fence();
+    }
+  }
+  template <bool Z = true, bool SPLIT = false>
+  static __device__ __forceinline__ void mac(uint32_t, uint32_t tab, const uint4& x, Acc& a) {
+    static_assert(Z, "eight-row tables live at LDS 0");
+    mac_dword(tab, x.x, a.s[0], a.s[1]);
+    mac_dword(tab, x.y, a.s[2], a.s[3]);
+    mac_dword(tab, x.z, a.s[4], a.s[5]);
+    mac_dword(tab, x.w, a.s[6], a.s[7]);
+  }
+  static __device__ __forceinline__ uint32_t pack(const v4u& lo, const v4u& hi, int r) {
+    const uint32_t a = r < 2 ? lo.x : r < 4 ? lo.y : r < 6 ? lo.z : lo.w;
+    const uint32_t b = r < 2 ? hi.x : r < 4 ? hi.y : r < 6 ? hi.z : hi.w;
+    return __builtin_amdgcn_perm(b, a, (r & 1) ? 0x07060302u : 0x05040100u);
+  }
   static __device__ __forceinline__ uint4 row(const Acc& a, int r) {
     return make_uint4(pack(a.s[0], a.s[1], r), pack(a.s[2], a.s[3], r), pack(a.s[4], a.s[5], r),
                       pack(a.s[6], a.s[7], r));
@@ -639,6 +703,18 @@ __device__ __forceinline__ void enc_item_pos(const EncodeParams& p, uint32_t w, 
   x = (w - o * p.tiles) * (kTile * CH) + wave_in_block() * (kChunkBytes * CH);
 }
 
+// Parity row q's store descriptor.  An eight-row pass (Gf16x8, m = 5..7)
+// computes rows past m from zero coefficients: their stores go through a
+// zero-record descriptor and are dropped, so every item still issues the
+// same instructions.
+template <int NR>
+__device__ __forceinline__ Rsrc parity_row(const EncodeParams& p, uint32_t o, int q, Rsrc par) {
+  if constexpr (NR > kRowsPerPass)
+    return rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride,
+                static_cast<uint32_t>(q) < p.nrows ? -1 : 0);
+  return par;
+}
+
 // Inputs an edge item holds in registers at once (edge items run inside the
 // streaming kernels, ahead of their interior items).
 constexpr int kEdgeGroup = 1;
@@ -688,7 +764,8 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
   const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
 #pragma unroll
   for (int q = 0; q < NR; ++q)
-    buf_st(par, t, (p.row0 + q) * p.frag_stride + kHeaderBytes, zero_tail(F::row(s, q), rem));
+    buf_st(parity_row<NR>(p, o, q, par), t, (p.row0 + q) * p.frag_stride + kHeaderBytes,
+           zero_tail(F::row(s, q), rem));
 }
 
 // Interior encode: object slices streamed in (default cache policy --
@@ -705,8 +782,21 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
 // wave takes CH KiB contiguous of every slice; the stream runs chunk-major
 // (the K inputs of chunk 0, its parity stores, then chunk 1 ...), so the
 // registers stay those of CH = 1.  NTL: nontemporal input loads.
+//
+// Prologue (HEAD).  The first NB loads are issued as the refills of a
+// previous item's last NB slots would be, with that item's stores -- data
+// fragment stores, then the NR parity stores -- through a zero-record
+// descriptor (no memory access).  hipcc computes one s_waitcnt per
+// instruction for every path into the loop head: with the stores missing on
+// the entry path, the wait for input 0 was vmcnt(4) there, and the steady
+// state (where the 4 parity stores are the youngest operations) inherited
+// it, so every wave drained all NB of its in-flight loads at every item
+// boundary (round 4, found in the generated code).  With the entry path
+// shaped like the back edge the wait is vmcnt(NB - 1 + NR (+ data stores)),
+// and loads stay in flight across items.  HEAD = false keeps the old
+// prologue (A/B builds).
 template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false, int CH = 1,
-          bool NTL = false, int NBX = 0>
+          bool NTL = false, int NBX = 0, bool HEAD = true>
 __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
   constexpr int NB = NBX ? NBX : stream_bufs<K>();  // NBX: A/B (divides K)
   const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split, interior_block(p.edge_blocks));
@@ -719,9 +809,17 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
   constexpr int KP = stream_slots<K, NB>();
   constexpr int SL = KP * CH;  // stream slots per item: slot i = chunk i / KP, input i % KP
   uint4 buf[NB];
+  const Rsrc none = rsrc(p.parity, 0);
+  const uint4 zero4 = make_uint4(0, 0, 0, 0);
 #pragma unroll
-  for (int j = 0; j < NB; ++j)
+  for (int j = 0; j < NB; ++j) {
+    if constexpr (HEAD && DATA)
+      if ((SL - NB + j) % KP < K) buf_st(none, lane16, 0, zero4);
     if (j < K) buf[j] = buf_ld<!NTL>(cur, lane16, j * p.bs + x);
+  }
+  if constexpr (HEAD)
+#pragma unroll
+    for (int q = 0; q < NR; ++q) buf_st(none, lane16, 0, zero4);
   // one item per trip: hipcc would otherwise unroll the item loop for small k
   // (k = 2..6: 256 VGPRs unconstrained, up to 1.4 KB per lane of spills at 64)
 #pragma clang loop unroll(disable)
@@ -762,7 +860,8 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
         F::pin(s);
         const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x + kChunkBytes * c;
 #pragma unroll
-        for (int q = 0; q < NR; ++q) buf_st(par, lane16, soff + q * p.frag_stride, F::row(s, q));
+        for (int q = 0; q < NR; ++q)
+          buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, F::row(s, q));
         if (c + 1 < CH) F::zero(s);
       }
     }
@@ -800,6 +899,7 @@ __device__ __forceinline__ void encode_edges(const EncodeParams& p, uint32_t fir
 // lane at 64 VGPRs and gets 72.
 template <class F, int K, bool DATA, int NBX>
 __host__ __device__ constexpr int encode_occ() {
+  if (F::kRows > kRowsPerPass) return 4;  // eight-row accumulators: 32 VGPRs
   if (DATA) return kEncodeDataOcc;
   if (NBX > 6) return 4;
   if (F::kW == 8 && K >= 18) return 7;
@@ -807,7 +907,7 @@ __host__ __device__ constexpr int encode_occ() {
 }
 
 template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false, int CH = 1,
-          bool NTL = false, int NBX = 0>
+          bool NTL = false, int NBX = 0, bool HEAD = true>
 __global__ void __launch_bounds__(kThreadsPerBlock)
     __attribute__((amdgpu_waves_per_eu(encode_occ<F, K, DATA, NBX>(), 8)))
     encode_kernel(EncodeParams p) {
@@ -821,7 +921,7 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
       return;
     }
   }
-  encode_interior<F, K, NR, NOCOMP, DATA, CH, NTL, NBX>(p);
+  encode_interior<F, K, NR, NOCOMP, DATA, CH, NTL, NBX, HEAD>(p);
 }
 
 // Headers and edge items of an encode in a launch of their own (the
@@ -924,9 +1024,17 @@ __device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
   const uint32_t lane16 = lane_id() * 16;
   constexpr int KP = stream_slots<K, NB>();
   uint4 buf[NB];
+  // prologue shaped like the back edge (see encode_interior, HEAD)
+  const Rsrc none = rsrc(p.parity, 0);
+  const uint4 zero4 = make_uint4(0, 0, 0, 0);
 #pragma unroll
-  for (int j = 0; j < NB; ++j)
+  for (int j = 0; j < NB; ++j) {
+    if constexpr (DATA)
+      if (KP - NB + j < K) buf_st(none, lane16, 0, zero4);
     if (j < K) buf[j] = buf_ld<!NTL>(cur, lane16, j * p.bs + x);
+  }
+#pragma unroll
+  for (int q = 0; q < NR; ++q) buf_st(none, lane16, 0, zero4);
   uint32_t acc[NR];
 #pragma unroll
   for (int q = 0; q < NR; ++q) acc[q] = 0;
@@ -1131,11 +1239,28 @@ static_assert(offsetof(ObjDesc, out_idx) == 32 && offsetof(ObjDesc, n_out) == 36
                   offsetof(ObjDesc, copy_inputs) == 37 && offsetof(ObjDesc, table) == 40 &&
                   offsetof(ObjDesc, header) == 44 && sizeof(ObjDesc) % 4 == 0,
               "DescU mirrors ObjDesc");
+// S (default): through the constant address space, so hipcc issues scalar
+// loads (s_load_dwordx8 + x4, counted by lgkmcnt) -- the descriptors are
+// written by the host before the launch and never by a kernel.  As vector
+// loads (S = false, the form up to round 3) they were counted by vmcnt
+// behind the item's in-flight payload loads and stores, and the wait for
+// them at every item boundary (vmcnt(0): the descriptor is the youngest
+// load) drained the whole stream (round 4, found in the generated code).
+typedef const __attribute__((address_space(4))) uint32_t const_u32;
+template <bool S = true>
 __device__ __forceinline__ DescU load_desc(const DecodeParams& p, uint32_t o) {
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(p.desc + o);
   DescU u;
+  if constexpr (S) {
+    const const_u32* src =
+        reinterpret_cast<const const_u32*>(reinterpret_cast<uintptr_t>(p.desc + o));
 #pragma unroll
-  for (uint32_t i = 0; i < sizeof(ObjDesc) / 4; ++i) u.w[i] = __builtin_amdgcn_readfirstlane(src[i]);
+    for (uint32_t i = 0; i < sizeof(ObjDesc) / 4; ++i) u.w[i] = src[i];
+  } else {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(p.desc + o);
+#pragma unroll
+    for (uint32_t i = 0; i < sizeof(ObjDesc) / 4; ++i)
+      u.w[i] = __builtin_amdgcn_readfirstlane(src[i]);
+  }
   return u;
 }
 
@@ -1170,7 +1295,7 @@ __device__ __forceinline__ Rsrc rsrc_out(const void* base) {
 // Stores that do not apply (parity inputs, rows past n_out) go to voffset
 // kDrop and are discarded by the range check, so every item issues the same
 // memory instructions.  NOCOMP: memory-only probe (no lookups; wrong rows).
-template <class F, int K, int MODE, bool NOCOMP = false, int NBX = 0>
+template <class F, int K, int MODE, bool NOCOMP = false, int NBX = 0, bool SDESC = true>
 __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st,
                                                 TablePre<F, K>& pre) {
   constexpr int NB = NBX ? NBX : stream_bufs<K>();  // NBX: A/B (divides K)
@@ -1180,16 +1305,42 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
   const uint32_t lane16 = lane_id() * 16;
   uint32_t o, x;
   dec_item_pos(p, w, o, x);
-  DescU d = load_desc(p, o);
+  DescU d = load_desc<SDESC>(p, o);
   constexpr int KP = stream_slots<K, NB>();
   uint4 buf[NB];
-  {
+  if constexpr (SDESC) {
+    // Prologue shaped like the back edge (see encode_interior, HEAD): the
+    // table prefetch first, then the item's vector-memory sequence -- a
+    // (zero-record, no access) store for each data store and each refill of
+    // the current item, the real loads where the refills fetch the next
+    // item's first NB inputs, the row stores.  The table switch at the loop
+    // head then waits only for the prefetch; with the prefetch last on the
+    // entry path it waited vmcnt(0/1) there, and so in the steady state too,
+    // draining the stream at every table change -- every item in the bench
+    // (round 4, found in the generated code).
+    table_prefetch<F, K>(p, d.table(), d.n_out() != 0, pre);
+    const Rsrc first = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride);
+    const Rsrc none = rsrc(p.frags, 0);
+    const uint4 zero4 = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      if (MODE != kReconstruct && j < K) buf_st(none, lane16, 0, zero4);
+      if (j + NB < KP) {
+        if (j + NB < K) buf_st(none, lane16, 0, zero4);
+      } else if (j + NB - KP < K) {
+        buf[j % NB] =
+            buf_ld(first, lane16, in_pos(p, d, j + NB - KP) * p.frag_stride + kHeaderBytes + x);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < (MODE == kReconstruct ? 1 : F::kRows); ++q) buf_st(none, lane16, 0, zero4);
+  } else {  // the round-3 prologue (A/B builds)
     const Rsrc first = rsrc(p.frags + static_cast<uint64_t>(o) * p.stripe_stride);
 #pragma unroll
     for (int j = 0; j < NB; ++j)
       if (j < K) buf[j] = buf_ld(first, lane16, in_pos(p, d, j) * p.frag_stride + kHeaderBytes + x);
+    table_prefetch<F, K>(p, d.table(), d.n_out() != 0, pre);
   }
-  table_prefetch<F, K>(p, d.table(), d.n_out() != 0, pre);
   // one item per trip: hipcc would otherwise unroll the item loop for small k
   // (k = 2..6: 256 VGPRs unconstrained, up to 1.4 KB per lane of spills at 64)
 #pragma clang loop unroll(disable)
@@ -1197,7 +1348,7 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
     const uint32_t wn = w + r.step < r.end ? w + r.step : w;
     uint32_t on, xn;
     dec_item_pos(p, wn, on, xn);
-    const DescU dn = load_desc(p, on);
+    const DescU dn = load_desc<SDESC>(p, on);
     // rebuilt from the object index each trip rather than carried over from
     // the last trip's `nxt`: the loop-carried 128-bit descriptor was kept in
     // VGPRs, and every input load went through a waterfall loop (10 per item
@@ -1325,7 +1476,7 @@ __device__ __forceinline__ void decode_edges(const DecodeParams& p, uint32_t fir
 // counted from the end of the grid (see encode_kernel), then the interior
 // stream.  The interior's first table change goes into the LDS slot the edge
 // items did not use, behind a barrier, as between any two items.
-template <class F, int K, int MODE, bool NOCOMP = false, int NBX = 0>
+template <class F, int K, int MODE, bool NOCOMP = false, int NBX = 0, bool SDESC = true>
 __global__ void __launch_bounds__(kThreadsPerBlock)
     __attribute__((amdgpu_waves_per_eu(NBX > 6 ? 4 : kDecodeOcc, 8))) decode_kernel(DecodeParams p) {
   Slots st{0xFFFFFFFFu, 1u};
@@ -1338,7 +1489,7 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
       return;
     }
   }
-  decode_interior<F, K, MODE, NOCOMP, NBX>(p, st, pre);
+  decode_interior<F, K, MODE, NOCOMP, NBX, SDESC>(p, st, pre);
 }
 
 // The edge work in a launch of its own (side-stream variant, ECAMD_EDGE_SIDE=1).
@@ -1351,16 +1502,6 @@ __global__ void __launch_bounds__(kThreadsPerBlock) decode_edge_kernel(DecodePar
 
 // ---------------- launch ----------------
 
-inline int env_int(const char* name, int dflt) {
-  const char* v = std::getenv(name);
-  return (v == nullptr || *v == 0) ? dflt : std::atoi(v);
-}
-
-inline bool env_flag(const char* name, bool dflt) {
-  const char* v = std::getenv(name);
-  if (v == nullptr || *v == 0) return dflt;
-  return v[0] != '0';
-}
 
 // Blocks per CU that are resident at once: the occupancy API's answer capped
 // by the register file (512 VGPRs per lane per SIMD, one wave per SIMD per
@@ -1368,14 +1509,17 @@ inline bool env_flag(const char* name, bool dflt) {
 // (MI355X_MICROARCH.md, Residency), and a grid-stride kernel must not queue
 // blocks behind the resident ones -- and by `max_per_cu`.
 inline int resident_per_cu(const void* kernel, size_t lds_bytes, int max_per_cu) {
-  // the hardware limit of a (kernel, LDS size) pair, asked once: the two
-  // runtime queries cost host time on every launch of a small call
+  // the hardware limit of a (device, kernel, LDS size) triple, asked once: the
+  // two runtime queries cost host time on every launch of a small call
   static std::mutex mu;
-  static std::map<std::pair<const void*, size_t>, int> limit;
+  static std::map<std::tuple<int, const void*, size_t>, int> limit;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  const auto key = std::make_tuple(dev, kernel, lds_bytes);
   int hw = 0;
   {
     std::lock_guard<std::mutex> lk(mu);
-    auto it = limit.find({kernel, lds_bytes});
+    auto it = limit.find(key);
     if (it != limit.end()) hw = it->second;
   }
   if (hw == 0) {
@@ -1389,7 +1533,7 @@ inline int resident_per_cu(const void* kernel, size_t lds_bytes, int max_per_cu)
     if (hipFuncGetAttributes(&attr, kernel) == hipSuccess && attr.numRegs > 0)
       hw = std::min(hw, 512 / ((attr.numRegs + 7) / 8 * 8));
     std::lock_guard<std::mutex> lk(mu);
-    limit[{kernel, lds_bytes}] = hw;
+    limit[key] = hw;
   }
   return std::max(std::min(max_per_cu, hw), 1);
 }
@@ -1430,6 +1574,11 @@ inline bool lds_starts_at_zero(const void* kern) {
   return ok;
 }
 
+// XCD-major work split (item_range) for a grid of `grid` blocks.
+inline uint32_t xcd_split_for(int grid, bool xcd) {
+  return (grid >= 8 && grid % 8 == 0 && ab_knob("ECAMD_XCD", xcd)) ? 1u : 0u;
+}
+
 template <typename Kern, typename Params>
 hipError_t launch(Kern kern, Params p, size_t lds, uint32_t items, hipStream_t stream,
                   int max_per_cu = 4, bool xcd = true, int* grid_out = nullptr) {
@@ -1437,7 +1586,7 @@ hipError_t launch(Kern kern, Params p, size_t lds, uint32_t items, hipStream_t s
   const void* k = reinterpret_cast<const void*>(kern);
   if (!lds_starts_at_zero(k)) return hipErrorInvalidKernelFile;
   const int grid = grid_for(k, lds, items, max_per_cu);
-  p.xcd_split = (grid >= 8 && grid % 8 == 0 && env_flag("ECAMD_XCD", xcd)) ? 1u : 0u;
+  p.xcd_split = xcd_split_for(grid, xcd);
   if (grid_out) *grid_out = grid;
 
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kThreadsPerBlock), lds, stream, p);
@@ -1448,14 +1597,13 @@ hipError_t launch(Kern kern, Params p, size_t lds, uint32_t items, hipStream_t s
 // the edge items (E = their count rounded up to 8, at most one per CU) and
 // return; blocks [E, E + G) stream the interior items exactly as a launch of
 // G blocks would.  All E + G blocks must be resident at once -- otherwise
-// interior blocks would queue behind the edge blocks -- else (or with
-// ECAMD_EDGE_BLOCKS=0) every block runs its share of the edge items first.
+// interior blocks would queue behind the edge blocks -- else (or with the
+// caller's no_edge_blocks) every block runs its share of the edge items first.
 // Why: an edge item is a chain of K dependent loads (one input in registers
 // at a time), ~12 us; with the edges at the front of some interior blocks,
 // those blocks finish that much after the rest (measured round 3 at 2 blocks
 // per CU, 256 x 4 MiB k = 10: encode 297.7 us fused, 291.0 with the edges
 // in a launch of their own before it, 284.7 for the interior alone).
-constexpr bool kEdgeBlocks = true;
 template <typename Kern, typename Params>
 hipError_t launch_edges_apart(Kern kern, Params p, size_t lds, uint32_t interior_items,
                               uint32_t edge_items, hipStream_t stream, int max_per_cu, bool xcd,
@@ -1464,8 +1612,7 @@ hipError_t launch_edges_apart(Kern kern, Params p, size_t lds, uint32_t interior
   const void* k = reinterpret_cast<const void*>(kern);
   const int cus = device_cus();
   const uint32_t e = (std::min<uint32_t>(edge_items, static_cast<uint32_t>(cus)) + 7u) & ~7u;
-  if (!env_flag("ECAMD_EDGE_BLOCKS", kEdgeBlocks) || edge_items == 0 || interior_items == 0 ||
-      !lds_starts_at_zero(k))
+  if (p.no_edge_blocks || edge_items == 0 || interior_items == 0 || !lds_starts_at_zero(k))
     return launch(kern, p, lds, std::max(interior_items, edge_items), stream, max_per_cu, xcd,
                   grid_out);
   const int grid = grid_for(k, lds, interior_items, max_per_cu);
@@ -1474,25 +1621,23 @@ hipError_t launch_edges_apart(Kern kern, Params p, size_t lds, uint32_t interior
     return launch(kern, p, lds, std::max(interior_items, edge_items), stream, max_per_cu, xcd,
                   grid_out);
   p.edge_blocks = e;
-  p.xcd_split = (grid >= 8 && grid % 8 == 0 && env_flag("ECAMD_XCD", xcd)) ? 1u : 0u;
+  p.xcd_split = xcd_split_for(grid, xcd);
   if (grid_out) *grid_out = grid;
   hipLaunchKernelGGL(kern, dim3(grid + static_cast<int>(e)), dim3(kThreadsPerBlock), lds, stream, p);
   return hipGetLastError();
 }
 
-// Side stream for the small launches of a call (headers, edge items): they
-// write bytes the interior launch does not touch, so they run beside it --
-// forked from and joined back into the caller's stream with events -- and
-// fill CUs the interior grid leaves idle (its tail; decode's spare wave
-// slots) instead of adding their latency in front of it (measured round 2:
-// 12 us encode / 15 us decode in series, rocprof r02h).
+// A/B builds only (ECAMD_EDGE_SIDE): the round-2 launch forms with the edge
+// items in a launch of their own, forked onto a side stream and joined back
+// with events (=1) or launched first on the same stream (=2).  Measured round
+// 2 (rocprof timeline, profiles/r02l_timeline.txt): the fork / join left the
+// GPU idle 25-32 us between consecutive interior kernels, hence the fused
+// launch of the product.
 struct SideStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
 };
 
-// Run main(stream) and side(side stream) concurrently, both after the work
-// already queued on `stream`; later work on `stream` waits for both.
 template <class Main, class Side>
 hipError_t fork_join(hipStream_t stream, Main main, Side side) {
   static std::mutex mu;
@@ -1500,7 +1645,7 @@ hipError_t fork_join(hipStream_t stream, Main main, Side side) {
   std::lock_guard<std::mutex> lk(mu);
   int dev = 0;
   SideStream* sd = nullptr;
-  if (env_int("ECAMD_EDGE_SIDE", 0) == 2) {  // A/B: edge launch first, same stream
+  if (ab_knob("ECAMD_EDGE_SIDE", 0) == 2) {
     const hipError_t e = side(stream);
     return e != hipSuccess ? e : main(stream);
   }
@@ -1537,10 +1682,6 @@ inline int64_t last_room(uint32_t bs, uint64_t obj_len, uint32_t k) {
   return room < 0 ? 0 : room;
 }
 
-// Encode: headers + edge items, then the interior stream, then (optionally)
-// the data fragments.  Interior tiles: 4 KiB of positions ending at or before
-// min(bs, room).  ECAMD_ENC_NOCOMP=1: memory-only probe of the benchmark
-// shape (tools/ab_bench.py).
 // Interior items of `ch` * 4 KiB: the tiles and the 4-KiB edge tiles past them.
 inline void set_tiles(EncodeParams& p, int64_t room, uint32_t ch) {
   p.tile_ch = ch;
@@ -1548,6 +1689,114 @@ inline void set_tiles(EncodeParams& p, int64_t room, uint32_t ch) {
   p.edge_tiles = (p.bs + kTile - 1) / kTile - p.tiles * ch;
 }
 
+// The inline_crc32 encode: one encode launch with the parity CRC fused, then
+// the finishing pass over the run partials.
+template <class F, int K, int NR, class Kern>
+hipError_t launch_encode_crc(EncodeParams p, Kern kern, int per_cu, uint32_t edge_items,
+                             hipStream_t stream) {
+  p.fused_edges = 1;
+  int grid = 0;
+  const hipError_t e = launch_edges_apart(kern, p, crc_lds_bytes<F, K>(), p.n_obj * p.tiles,
+                                          edge_items, stream, per_cu, false, &grid);
+  if (e != hipSuccess) return e;
+  CrcFinishParams fp{};
+  fp.parity = p.parity;
+  fp.frag_stride = p.frag_stride;
+  fp.stripe_stride = p.stripe_stride;
+  fp.part = p.crc_part;
+  fp.maps = p.crc_tables;
+  fp.tables = p.crc_finish_tables;
+  fp.n_obj = p.n_obj;
+  fp.m = p.m;
+  fp.row0 = p.row0;
+  fp.nrows = NR;
+  fp.bs = p.bs;
+  fp.tiles = p.tiles;
+  fp.edge_tiles = p.edge_tiles;
+  fp.grid = static_cast<uint32_t>(grid);
+  return launch_crc_finish(fp, stream);
+}
+
+// A/B builds: the alternative encode launches of past measurements (the
+// switches are documented where each one was measured: DESIGN.md §4).
+// Returns hipErrorNotSupported when no switch applies to this launch.
+template <class F, int K, int NR>
+hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint32_t edge_items) {
+  const int64_t room = last_room(p.bs, p.obj_len, K);
+  constexpr size_t lds = K * F::kTableBytes;
+  const int per_cu = ab_knob("ECAMD_ENC_PER_CU", kEncodePerCu);
+  if (p.crc_tables != nullptr) {
+    const int crc_per_cu = ab_knob("ECAMD_CRC_PER_CU", kEncodePerCu);
+    if constexpr (K == 10 && NR == 4)
+      if (!data && ab_knob("ECAMD_CRC_NTL", 0))
+        return launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR, false, true>, crc_per_cu,
+                                           edge_items, stream);
+    if (crc_per_cu != kEncodePerCu)
+      return data ? launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR, true>, crc_per_cu,
+                                                edge_items, stream)
+                  : launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR>, crc_per_cu,
+                                                edge_items, stream);
+    return hipErrorNotSupported;
+  }
+  if (ab_knob("ECAMD_EDGE_SIDE", 0)) {
+    p.fused_edges = 0;
+    hipError_t e = fork_join(
+        stream,
+        [&](hipStream_t s) { return launch(encode_kernel<F, K, NR>, p, lds, p.n_obj * p.tiles, s, per_cu); },
+        [&](hipStream_t s) {
+          return launch(encode_edge_kernel<F, K, NR>, p, lds,
+                        std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u), s);
+        });
+    if (e != hipSuccess || !data) return e;
+    return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + kTile - 1) / kTile), stream);
+  }
+  p.fused_edges = 1;
+  const uint32_t items = p.n_obj * p.tiles;
+  if (data && ab_knob("ECAMD_DATA_COPY", 0)) {
+    const hipError_t e = launch_edges_apart(encode_kernel<F, K, NR>, p, lds, items, edge_items,
+                                            stream, per_cu, true);
+    if (e != hipSuccess) return e;
+    return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + kTile - 1) / kTile), stream);
+  }
+  if constexpr (K == 10 && NR == 4) {
+    const bool ntl = ab_knob("ECAMD_ENC_NTL", 0);
+    if (ab_knob("ECAMD_ENC_NOCOMP", 0))  // memory-only probe: WRONG parity
+      return ntl ? launch_edges_apart(encode_kernel<F, K, NR, true, false, 1, true>, p, lds, items,
+                                      edge_items, stream, per_cu, true)
+                 : launch_edges_apart(encode_kernel<F, K, NR, true>, p, lds, items, edge_items,
+                                      stream, per_cu, true);
+    if (!data) {
+      if (ab_knob("ECAMD_ENC_R3", 0))  // the round-3 prologue (item-boundary drain)
+        return launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, false, 0, false>, p, lds,
+                                  items, edge_items, stream, per_cu, true);
+      const int ch = ab_knob("ECAMD_ENC_CH", 1);
+      const int nb = ab_knob("ECAMD_ENC_NB", 0);  // 10: every input of an item in flight
+      if (nb == 10)
+        return ntl ? launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, true, 10>, p, lds, items, edge_items, stream, per_cu, true)
+                   : launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, false, 10>, p, lds, items, edge_items, stream, per_cu, true);
+      if (ch == 2) {
+        set_tiles(p, room, 2);
+        const uint32_t items2 = p.n_obj * p.tiles;
+        const uint32_t edges2 = std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u);
+        return ntl ? launch_edges_apart(encode_kernel<F, K, NR, false, false, 2, true>, p, lds, items2, edges2, stream, per_cu, true)
+                   : launch_edges_apart(encode_kernel<F, K, NR, false, false, 2, false>, p, lds, items2, edges2, stream, per_cu, true);
+      }
+      if (ntl)
+        return launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, true>, p, lds, items,
+                                  edge_items, stream, per_cu, true);
+    }
+  }
+  if (per_cu != kEncodePerCu)
+    return data ? launch_edges_apart(encode_kernel<F, K, NR, false, true>, p, lds, items,
+                                     edge_items, stream, per_cu, true)
+                : launch_edges_apart(encode_kernel<F, K, NR>, p, lds, items, edge_items, stream,
+                                     per_cu, true);
+  return hipErrorNotSupported;
+}
+
+// Encode: one launch -- interior stream + edge items + headers, and the data
+// fragments when asked (stored from the input registers) -- or, with
+// inline_crc32, the CRC-fused launch and its finishing pass.
 template <class F, int K, int NR>
 hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   const int64_t room = last_room(p.bs, p.obj_len, K);
@@ -1555,105 +1804,29 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   constexpr size_t lds = K * F::kTableBytes;
   // data fragments are written by the first pass (rows 0..3) only
   const bool data = p.data != nullptr && p.row0 == 0;
-  bool probe = false;
-  const int per_cu = env_int("ECAMD_ENC_PER_CU", kEncodePerCu);  // A/B
   // interior and edge work items (edge items include the headers' objects)
   const uint32_t edge_items = std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u);
-  if constexpr (K == 10 && NR == 4) {
-    probe = env_flag("ECAMD_ENC_NOCOMP", false);
-    // A/B: CH KiB per wave and slice (ECAMD_ENC_CH=2), nontemporal loads
-    // (ECAMD_ENC_NTL=1); plain encode (no CRC, no data fragments) only
-    const int ch = env_int("ECAMD_ENC_CH", 1);
-    const bool ntl = env_flag("ECAMD_ENC_NTL", false);
-    const int nb = env_int("ECAMD_ENC_NB", 0);  // 10: every input of an item in flight
-    if (p.crc_tables == nullptr && !data && !probe && (ch == 2 || ntl || nb == 10) &&
-        !env_flag("ECAMD_EDGE_SIDE", false)) {
-      p.fused_edges = 1;
-      if (ch == 2) set_tiles(p, room, 2);
-      const uint32_t items = p.n_obj * p.tiles;
-      const uint32_t edges = std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u);
-      if (nb == 10)
-        return ntl ? launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, true, 10>, p, lds, items, edges, stream, per_cu, true)
-                   : launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, false, 10>, p, lds, items, edges, stream, per_cu, true);
-      if (ch == 2)
-        return ntl ? launch_edges_apart(encode_kernel<F, K, NR, false, false, 2, true>, p, lds, items, edges, stream, per_cu, true)
-                   : launch_edges_apart(encode_kernel<F, K, NR, false, false, 2, false>, p, lds, items, edges, stream, per_cu, true);
-      return launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, true>, p, lds, items, edges, stream, per_cu, true);
-    }
+  if constexpr (kAB && F::kRows <= kRowsPerPass) {
+    const hipError_t e = launch_encode_ab<F, K, NR>(p, stream, data, edge_items);
+    if (e != hipErrorNotSupported) return e;
   }
-  hipError_t e;
   if (p.crc_tables != nullptr) {
-    // inline_crc32 with the parity CRC fused: one encode launch + the
-    // finishing pass over the run partials
-    p.fused_edges = 1;
-    const uint32_t items = p.n_obj * p.tiles;
-    int grid = 0;
-    const int crc_per_cu = env_int("ECAMD_CRC_PER_CU", kEncodePerCu);  // A/B knob
-    bool crc_ntl = false;
-    if constexpr (K == 10 && NR == 4) {
-      crc_ntl = !data && env_flag("ECAMD_CRC_NTL", false);  // A/B
-      if (crc_ntl)
-        e = launch_edges_apart(encode_crc_kernel<F, K, NR, false, true>, p, crc_lds_bytes<F, K>(),
-                               items, edge_items, stream, crc_per_cu, false, &grid);
+    if constexpr (F::kRows > kRowsPerPass) {
+      return hipErrorInvalidValue;  // the fused CRC runs in four-row passes
+    } else {
+      return data ? launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR, true>, kEncodePerCu,
+                                                edge_items, stream)
+                  : launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR>, kEncodePerCu,
+                                                edge_items, stream);
     }
-    if (!crc_ntl)
-      e = data ? launch_edges_apart(encode_crc_kernel<F, K, NR, true>, p, crc_lds_bytes<F, K>(),
-                                    items, edge_items, stream, crc_per_cu, false, &grid)
-               : launch_edges_apart(encode_crc_kernel<F, K, NR>, p, crc_lds_bytes<F, K>(), items,
-                                    edge_items, stream, crc_per_cu, false, &grid);
-    if (e != hipSuccess) return e;
-    CrcFinishParams fp{};
-    fp.parity = p.parity;
-    fp.frag_stride = p.frag_stride;
-    fp.stripe_stride = p.stripe_stride;
-    fp.part = p.crc_part;
-    fp.maps = p.crc_tables;
-    fp.tables = p.crc_finish_tables;
-    fp.n_obj = p.n_obj;
-    fp.m = p.m;
-    fp.row0 = p.row0;
-    fp.nrows = NR;
-    fp.bs = p.bs;
-    fp.tiles = p.tiles;
-    fp.edge_tiles = p.edge_tiles;
-    fp.grid = static_cast<uint32_t>(grid);
-    return launch_crc_finish(fp, stream);
   }
-  if (!env_flag("ECAMD_EDGE_SIDE", false)) {
-    // one launch: interior stream + edge items + headers (+ the data
-    // fragments when asked: stored from the input registers)
-    p.fused_edges = 1;
-    const uint32_t items = p.n_obj * p.tiles;
-    if constexpr (K == 10 && NR == 4)
-      if (probe)
-        return env_flag("ECAMD_ENC_NTL", false)
-                   ? launch_edges_apart(encode_kernel<F, K, NR, true, false, 1, true>, p, lds, items,
-                                        edge_items, stream, per_cu, true)
-                   : launch_edges_apart(encode_kernel<F, K, NR, true>, p, lds, items, edge_items,
-                                        stream, per_cu, true);
-    if (data && !env_flag("ECAMD_DATA_COPY", false))
-      return launch_edges_apart(encode_kernel<F, K, NR, false, true>, p, lds, items, edge_items,
-                                stream, per_cu, true);
-    e = launch_edges_apart(encode_kernel<F, K, NR>, p, lds, items, edge_items, stream, per_cu, true);
-    if (e != hipSuccess || !data) return e;
-    // ECAMD_DATA_COPY=1 (A/B): the data fragments in a copy launch of their own
-    return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + kTile - 1) / kTile), stream);
-  }
-  p.fused_edges = 0;
-  e = fork_join(
-      stream,
-      [&](hipStream_t s) {
-        if constexpr (K == 10 && NR == 4)
-          if (probe)
-            return launch(encode_kernel<F, K, NR, true>, p, lds, p.n_obj * p.tiles, s, per_cu);
-        return launch(encode_kernel<F, K, NR>, p, lds, p.n_obj * p.tiles, s, per_cu);
-      },
-      [&](hipStream_t s) {
-        return launch(encode_edge_kernel<F, K, NR>, p, lds,
-                      std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u), s);
-      });
-  if (e != hipSuccess || !data) return e;
-  return launch(copy_data_kernel, p, 0, p.n_obj * K * ((p.bs + kTile - 1) / kTile), stream);
+  p.fused_edges = 1;
+  const uint32_t items = p.n_obj * p.tiles;
+  if (data)
+    return launch_edges_apart(encode_kernel<F, K, NR, false, true>, p, lds, items, edge_items,
+                              stream, kEncodePerCu, true);
+  return launch_edges_apart(encode_kernel<F, K, NR>, p, lds, items, edge_items, stream,
+                            kEncodePerCu, true);
 }
 
 template <class F, int K>
@@ -1678,10 +1851,47 @@ constexpr uint32_t decode_lds_bytes() {
   return 2 * table_slot_bytes(K, F::kW);
 }
 
+// A/B builds: the alternative decode launches (see launch_encode_ab).
+template <class F, int K, int MODE>
+hipError_t launch_decode_ab(DecodeParams p, hipStream_t stream, uint32_t edge_items) {
+  constexpr size_t lds = decode_lds_bytes<F, K>();
+  const int per_cu = MODE == kReconstruct ? ab_knob("ECAMD_REC_PER_CU", kReconstructPerCu)
+                                          : ab_knob("ECAMD_DEC_PER_CU", kDecodePerCu);
+  if (ab_knob("ECAMD_EDGE_SIDE", 0)) {
+    p.fused_edges = 0;
+    return fork_join(
+        stream,
+        [&](hipStream_t s) {
+          return launch(decode_kernel<F, K, MODE>, p, lds, p.n_obj * p.tiles, s, per_cu, kDecodeXcd);
+        },
+        [&](hipStream_t s) { return launch(decode_edge_kernel<F, K, MODE>, p, lds, edge_items, s); });
+  }
+  p.fused_edges = 1;
+  const uint32_t items = p.n_obj * p.tiles;
+  if constexpr (K == 10 && MODE == kDecode) {
+    if (ab_knob("ECAMD_DEC_NOCOMP", 0))  // memory-only probe: WRONG objects
+      return launch_edges_apart(decode_kernel<F, K, MODE, true>, p, lds, items, edge_items, stream,
+                                per_cu, kDecodeXcd);
+    if (ab_knob("ECAMD_DEC_R3", 0))  // round 3: vector descriptor loads, old prologue
+      return launch_edges_apart(decode_kernel<F, K, MODE, false, 0, false>, p, lds, items,
+                                edge_items, stream, per_cu, kDecodeXcd);
+    const int nb = ab_knob("ECAMD_DEC_NB", 0);  // inputs in flight per wave
+    if (nb == 10)
+      return launch_edges_apart(decode_kernel<F, K, MODE, false, 10>, p, lds, items, edge_items,
+                                stream, per_cu, kDecodeXcd);
+    if (nb == 2)
+      return launch_edges_apart(decode_kernel<F, K, MODE, false, 2>, p, lds, items, edge_items,
+                                stream, per_cu, kDecodeXcd);
+  }
+  if (per_cu != (MODE == kReconstruct ? kReconstructPerCu : kDecodePerCu))
+    return launch_edges_apart(decode_kernel<F, K, MODE>, p, lds, items, edge_items, stream, per_cu,
+                              kDecodeXcd);
+  return hipErrorNotSupported;
+}
+
 // Decode / reconstruct: (reconstruct headers +) edge items, then the
-// interior stream.  A multi-pass decode runs each pass as a decode (the
-// descriptor's copy_inputs / n_out say what the pass stores).
-// ECAMD_DEC_NOCOMP=1: memory-only probe of the benchmark shape.
+// interior stream, in one launch.  A multi-pass decode runs each pass as a
+// decode (the descriptor's copy_inputs / n_out say what the pass stores).
 template <class F, int K, int MODE>
 hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
   if constexpr (MODE == kDecodeGeneric) {
@@ -1694,40 +1904,14 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
     constexpr size_t lds = decode_lds_bytes<F, K>();
     const uint32_t edge_items =
         std::max(p.n_obj * p.edge_tiles, MODE == kReconstruct && p.headers ? p.n_obj : 0u);
-    bool probe = false;
-    if constexpr (K == 10 && MODE == kDecode) probe = env_flag("ECAMD_DEC_NOCOMP", false);
-    if (!env_flag("ECAMD_EDGE_SIDE", false)) {
-      p.fused_edges = 1;
-      const uint32_t items = p.n_obj * p.tiles;
-      const int per_cu = MODE == kReconstruct ? env_int("ECAMD_REC_PER_CU", kReconstructPerCu)
-                                              : env_int("ECAMD_DEC_PER_CU", kDecodePerCu);  // A/B
-      if constexpr (K == 10 && MODE == kDecode) {
-        if (probe)
-          return launch_edges_apart(decode_kernel<F, K, MODE, true>, p, lds, items, edge_items,
-                                    stream, per_cu, kDecodeXcd);
-        const int nb = env_int("ECAMD_DEC_NB", 0);  // A/B: inputs in flight per wave
-        if (nb == 10)
-          return launch_edges_apart(decode_kernel<F, K, MODE, false, 10>, p, lds, items, edge_items,
-                                    stream, per_cu, kDecodeXcd);
-        if (nb == 2)
-          return launch_edges_apart(decode_kernel<F, K, MODE, false, 2>, p, lds, items, edge_items,
-                                    stream, per_cu, kDecodeXcd);
-      }
-      return launch_edges_apart(decode_kernel<F, K, MODE>, p, lds, items, edge_items, stream,
-                                per_cu, kDecodeXcd);
+    if constexpr (kAB) {
+      const hipError_t e = launch_decode_ab<F, K, MODE>(p, stream, edge_items);
+      if (e != hipErrorNotSupported) return e;
     }
-    p.fused_edges = 0;
-    return fork_join(
-        stream,
-        [&](hipStream_t s) {
-          if constexpr (K == 10 && MODE == kDecode)
-            if (probe)
-              return launch(decode_kernel<F, K, MODE, true>, p, lds, p.n_obj * p.tiles, s,
-                            kDecodePerCu, kDecodeXcd);
-          return launch(decode_kernel<F, K, MODE>, p, lds, p.n_obj * p.tiles, s, kDecodePerCu,
-                        kDecodeXcd);
-        },
-        [&](hipStream_t s) { return launch(decode_edge_kernel<F, K, MODE>, p, lds, edge_items, s); });
+    p.fused_edges = 1;
+    return launch_edges_apart(decode_kernel<F, K, MODE>, p, lds, p.n_obj * p.tiles, edge_items,
+                              stream, MODE == kReconstruct ? kReconstructPerCu : kDecodePerCu,
+                              kDecodeXcd);
   }
 }
 

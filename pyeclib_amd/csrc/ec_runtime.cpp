@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
@@ -30,6 +31,7 @@
 #include "erasurecode_amd.h"
 #include "gf16.hpp"
 #include "gf8.hpp"
+#include "host_copy.hpp"
 
 namespace ecamd {
 namespace {
@@ -83,15 +85,49 @@ inline uint64_t get64(const void* p) {
   return v;
 }
 
-bool env_on(const char* name) {
+bool env_on(const char* name, bool dflt = false) {
   const char* v = std::getenv(name);
-  return v != nullptr && v[0] != 0 && v[0] != '0';
+  if (v == nullptr || v[0] == 0) return dflt;
+  return v[0] != '0';
 }
 
-int env_int(const char* name, int dflt) {
+long env_long(const char* name, long dflt) {
   const char* v = std::getenv(name);
-  return (v == nullptr || *v == 0) ? dflt : std::atoi(v);
+  return (v == nullptr || *v == 0) ? dflt : std::atol(v);
 }
+
+// Runtime knobs, read from the environment once, when an instance is created
+// -- never on the call path.  Each one selects between outputs that are
+// identical (a staging path, a pool size, a launch form); none changes a byte
+// written.  Tests and tools/ use them to reach every path.
+struct Knobs {
+  // objects up to this many bytes take the zero-copy single-object path (0:
+  // never).  Measured round 2 (tools/single_ab.py, profiles/r02m_single_ab.txt
+  // and r02n, k=10 m=4): faster than the DMA path up to 1 MiB on both boxes
+  // -- 64 KiB encode 51-54 vs 97-105 us, decode 57-59 vs 91-93; 1 MiB 148 vs
+  // 181-187, 163-167 vs 264-268.
+  size_t single_pinned_max = size_t(1) << 20;  // ECAMD_SINGLE_PINNED_MAX
+  long pool_slots = 0;          // ECAMD_POOL_SLOTS: decode table-set slots (0 = from 32 MiB)
+  bool host_staged = false;     // ECAMD_HOST_STAGED: copy-engine host pipeline
+  bool host_staged_out = false; // ECAMD_HOST_STAGED_OUT: ... with outputs staged through HBM
+  int host_streams = 3;         // ECAMD_HOST_STREAMS
+  int host_chunk_mb = 32;       // ECAMD_HOST_CHUNK_MB
+  bool edge_blocks = true;      // ECAMD_EDGE_BLOCKS=0: the round-2 launch form
+  bool crc_fused = true;        // ECAMD_CRC_FUSED=0: parity CRC as a separate pass
+  static Knobs from_env() {
+    Knobs k;
+    k.single_pinned_max = static_cast<size_t>(
+        std::max<long>(0, env_long("ECAMD_SINGLE_PINNED_MAX", static_cast<long>(k.single_pinned_max))));
+    k.pool_slots = std::max<long>(0, env_long("ECAMD_POOL_SLOTS", 0));
+    k.host_staged = env_on("ECAMD_HOST_STAGED");
+    k.host_staged_out = env_on("ECAMD_HOST_STAGED_OUT");
+    k.host_streams = static_cast<int>(env_long("ECAMD_HOST_STREAMS", k.host_streams));
+    k.host_chunk_mb = static_cast<int>(std::max<long>(1, env_long("ECAMD_HOST_CHUNK_MB", k.host_chunk_mb)));
+    k.edge_blocks = env_on("ECAMD_EDGE_BLOCKS", true);
+    k.crc_fused = env_on("ECAMD_CRC_FUSED", true);
+    return k;
+  }
+};
 
 bool write_legacy_crc() {
   const char* v = std::getenv("LIBERASURECODE_WRITE_LEGACY_CRC");
@@ -204,18 +240,6 @@ struct PinBuf {
   }
 };
 
-// Objects up to this many bytes take the zero-copy single-object path
-// (ECAMD_SINGLE_PINNED_MAX overrides; 0 turns it off).  Measured round 2
-// (tools/single_ab.py, profiles/r02m_single_ab.txt and r02n, k=10 m=4):
-// faster than the DMA path up to 1 MiB on both boxes -- 64 KiB encode 51-54
-// vs 97-105 us, decode 57-59 vs 91-93; 1 MiB 148 vs 181-187, 163-167 vs
-// 264-268 -- and mixed at 4 MiB, where host-side copies and page faults
-// dominate either way.
-size_t single_pinned_max() {
-  const char* v = std::getenv("ECAMD_SINGLE_PINNED_MAX");
-  return (v == nullptr || *v == 0) ? (size_t(1) << 20) : static_cast<size_t>(std::atoll(v));
-}
-
 // Descriptor/header upload slot: pinned staging + device copy + completion event.
 struct RingSlot {
   uint8_t* host = nullptr;
@@ -239,14 +263,13 @@ struct UploadCache {
   uint8_t* host = nullptr;
   size_t host_cap = 0;
   DevBuf dev;
-  hipStream_t last_stream = nullptr;
-  bool used = false;          // last_stream is meaningful
   hipEvent_t fill_ev = nullptr;     // recorded after the H2D copy that filled `dev`
   hipStream_t fill_stream = nullptr;
   bool fill_done = false;           // that copy is known to be complete
-  bool multi_stream = false;  // read from more than one stream since filled
-  void release() {
-    if (used) (void)hipDeviceSynchronize();  // launches reading `dev` (no events)
+  // (launches that read `dev` record no event -- an event record costs GPU
+  // time between kernels; the instance's per-stream waits order a rewrite
+  // after them, Instance::order_after_streams)
+  void release() {  // the instance's streams are idle (~Instance)
     if (fill_ev) {
       (void)hipEventSynchronize(fill_ev);
       (void)hipEventDestroy(fill_ev);
@@ -264,14 +287,36 @@ struct Instance {
   int k = 0, m = 0, ct = CHKSUM_NONE, backend_id = 0, device = 0;
   Code code = kRsVand;
   bool legacy_crc = false;
+  Knobs knobs;
   uint32_t passes = 1;  // ceil(m / 4) table sets per decode pattern
   GfMatrix gen;
   std::mutex mu;
   hipStream_t stream = nullptr;
+  // Every stream a launch of this instance has been queued on (a caller's
+  // few streams, the instance's own).  A device buffer the instance rewrites
+  // or frees is read only by launches on these streams, so waiting for them
+  // -- on the GPU where the rewrite is itself queued, on the host where it is
+  // not -- replaces a device-wide synchronisation: other instances' and other
+  // threads' work is never waited for, and every error is returned.
+  // (Streams passed to ecamd_* calls must stay valid while the instance
+  // lives; include/erasurecode_amd.h.)
+  std::vector<hipStream_t> streams;
+  std::vector<hipEvent_t> stream_ev;  // one reusable marker per stream
   DevBuf enc_tables;  // passes x k x 64 u64
+  // GF(2^16) with 4 < m <= 8: one eight-row table set (k x 1 KiB), so encode
+  // reads the object once (ec_kernels_impl.hpp Gf16x8); the four-row passes
+  // above remain for the fused inline-CRC encode
+  bool wide = false;
+  DevBuf enc_tables8;
   DevBuf pool;        // decode / reconstruct table sets
   uint32_t pool_slots = 0, pool_used = 0;
   uint64_t pool_gen = 1;  // bumped whenever slots are recycled
+  // recorded where the pool was last recycled, after the waits for every
+  // launch that could read the old table sets: a table copy queued on
+  // another stream waits for it before overwriting a slot
+  hipEvent_t pool_gen_ev = nullptr;
+  hipStream_t pool_gen_stream = nullptr;
+  bool pool_gen_pending = false;
   std::unordered_map<uint64_t, uint32_t> pool_index;
   // table sets of patterns new in this call: built on the host into
   // pool_stage (slots pool_stage_first..), uploaded by pool_commit with ONE
@@ -282,6 +327,10 @@ struct Instance {
   hipEvent_t pool_ev = nullptr;
   hipStream_t pool_ev_stream = nullptr;
   bool pool_ev_pending = false;
+  // host-side phase times of the last single-object call (ecamd_call_phases):
+  // [0] copy in, [1] launch, [2] host work beside the kernel, [3] wait for
+  // the kernel, [4] copy out, [5] headers; microseconds
+  double phase_us[6] = {0, 0, 0, 0, 0, 0};
   DevBuf scratch;  // single-object staging
   PinBuf pin;      // single-object staging, zero-copy (small objects)
   RingSlot ring[kRing];
@@ -306,8 +355,42 @@ struct Instance {
   // bytes of one table set (k inputs x up to 4 rows)
   size_t table_bytes() const { return static_cast<size_t>(k) * table_bytes_per_input(code.w); }
 
+  // A launch of this instance is about to be queued on s.
+  hipError_t note_stream(hipStream_t s) {
+    for (hipStream_t t : streams)
+      if (t == s) return hipSuccess;
+    hipEvent_t ev = nullptr;
+    const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+    streams.push_back(s);
+    stream_ev.push_back(ev);
+    return hipSuccess;
+  }
+  // GPU-side: work queued on s from now on runs after everything queued so
+  // far on the instance's other streams (s's own work is ordered already).
+  hipError_t order_after_streams(hipStream_t s) {
+    for (size_t i = 0; i < streams.size(); ++i) {
+      if (streams[i] == s) continue;
+      hipError_t e = hipEventRecord(stream_ev[i], streams[i]);
+      if (e == hipSuccess) e = hipStreamWaitEvent(s, stream_ev[i], 0);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
+  // Host-side: wait for everything queued so far on the instance's streams.
+  hipError_t wait_streams() {
+    hipError_t first = hipSuccess;
+    for (size_t i = 0; i < streams.size(); ++i) {
+      hipError_t e = hipEventRecord(stream_ev[i], streams[i]);
+      if (e == hipSuccess) e = hipEventSynchronize(stream_ev[i]);
+      if (e != hipSuccess && first == hipSuccess) first = e;
+    }
+    return first;
+  }
+
   ~Instance() {
     DeviceGuard g(device);
+    (void)wait_streams();
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& s : hstream)
       if (s) {
@@ -316,6 +399,8 @@ struct Instance {
       }
     for (auto& e : hdone)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : stream_ev) (void)hipEventDestroy(e);
+    if (pool_gen_ev) (void)hipEventDestroy(pool_gen_ev);
     if (pool_ev) {
       (void)hipEventSynchronize(pool_ev);
       (void)hipEventDestroy(pool_ev);
@@ -332,6 +417,7 @@ struct Instance {
       r.dev.release();
     }
     enc_tables.release();
+    enc_tables8.release();
     pool.release();
     scratch.release();
     pin.release();
@@ -409,14 +495,15 @@ int upload(Instance& I, UploadCache& C, const std::vector<uint8_t>& key, uint64_
     return 0;
   }
   if (C.last_key == key && C.last_gen == gen) {
-    // second call in a row with this key: make it resident, once no launch
-    // can still be reading the old bytes
-    // (launches that read the cache record no event -- an event record costs
-    // GPU time between kernels -- so a rewrite waits for the whole device; it
-    // happens once per new repeated key)
-    if (C.used && (e = hipDeviceSynchronize()) != hipSuccess) return hip_errno(e);
-    C.multi_stream = false;
-    C.used = false;
+    // second call in a row with this key: make it resident.  The copy that
+    // rewrites `dev` is queued on s behind every launch of this instance
+    // that may still read the old bytes (launches that read the cache record
+    // no event: the GPU-side waits cover them, once per new repeated key),
+    // and the host staging buffer is rewritten only once its previous copy
+    // has completed.
+    if (C.dev_valid && (e = I.order_after_streams(s)) != hipSuccess) return hip_errno(e);
+    if (C.fill_ev && !C.fill_done && (e = hipEventSynchronize(C.fill_ev)) != hipSuccess)
+      return hip_errno(e);
     C.dev_valid = false;
     if (C.host_cap < n) {
       if (C.host) (void)hipHostFree(C.host);
@@ -458,20 +545,13 @@ int upload(Instance& I, UploadCache& C, const std::vector<uint8_t>& key, uint64_
 // After the launch(es) that read an Upload's bytes.
 hipError_t upload_done(Instance& I, Upload& u, hipStream_t s) {
   if (u.ring) return I.ring_release(u.ring, s);
-  if (u.cache) {
-    UploadCache& C = *u.cache;
-    if (C.used && C.last_stream != s) C.multi_stream = true;
-    C.last_stream = s;
-    C.used = true;
-    return hipSuccess;
-  }
   return hipSuccess;
 }
 
 // The fused parity CRC's partials buffer for launches on stream s, at least
 // `bytes` long.  A stream keeps its slot; a new stream takes a free slot, or
-// -- all taken -- the round-robin victim once the device is idle (its stream
-// may be gone).  Growing a slot waits for its own stream only.
+// -- all taken -- the round-robin victim, whose last user's queued work s
+// then waits for on the GPU.  Growing a slot waits for its own stream only.
 hipError_t crc_part_for(Instance& I, hipStream_t s, size_t bytes, uint32_t** out) {
   Instance::CrcPart* slot = nullptr;
   for (auto& c : I.crc_part)
@@ -489,7 +569,8 @@ hipError_t crc_part_for(Instance& I, hipStream_t s, size_t bytes, uint32_t** out
     if (!slot) {
       slot = &I.crc_part[I.crc_part_victim];
       I.crc_part_victim = (I.crc_part_victim + 1) % kCrcPartSlots;
-      if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+      // the victim's last stream is one of the instance's streams
+      if ((e = I.order_after_streams(s)) != hipSuccess) return e;
     }
     slot->stream = s;
     slot->used = true;
@@ -665,15 +746,24 @@ void missing_rows(const Instance& I, const int* avail, int dest, std::vector<int
     if (!present[j]) out_idx.push_back(j);
 }
 
-// Wait for every launch that may read the pool, then forget all patterns.
+// Forget all patterns; the next table copies into the pool (queued on s, the
+// recycling call's stream, or on any other stream after pool_gen_ev) run
+// after every launch queued so far that may read the old sets.  No host wait.
 // (Staged sets were committed by the flush that precedes every recycle.)
-void pool_recycle(Instance& I) {
-  (void)hipDeviceSynchronize();
+hipError_t pool_recycle(Instance& I, hipStream_t s) {
+  hipError_t e = I.order_after_streams(s);
+  if (e != hipSuccess) return e;
+  if (!I.pool_gen_ev && (e = hipEventCreateWithFlags(&I.pool_gen_ev, hipEventDisableTiming)) != hipSuccess)
+    return e;
+  if ((e = hipEventRecord(I.pool_gen_ev, s)) != hipSuccess) return e;
+  I.pool_gen_stream = s;
+  I.pool_gen_pending = true;
   I.pool_index.clear();
   I.pool_used = 0;
   I.pool_stage.clear();
   I.pool_ev_pending = false;
   ++I.pool_gen;
+  return hipSuccess;
 }
 
 int pool_slot(Instance& I, uint32_t avail_mask, const int* avail, int dest, uint32_t* slot,
@@ -689,9 +779,8 @@ int pool_slot(Instance& I, uint32_t avail_mask, const int* avail, int dest, uint
   const size_t set_bytes = I.table_bytes();
   if (I.pool_slots == 0) {
     const size_t slot_bytes = set_bytes * I.passes;
-    // ECAMD_POOL_SLOTS (tests): force a small pool to exercise recycling
-    const char* env = std::getenv("ECAMD_POOL_SLOTS");
-    const long forced = env ? std::atol(env) : 0;
+    // knob ECAMD_POOL_SLOTS (tests): force a small pool to exercise recycling
+    const long forced = I.knobs.pool_slots;
     I.pool_slots = forced > 0 ? static_cast<uint32_t>(forced)
                               : static_cast<uint32_t>(
                                     std::max<size_t>(64, (size_t(32) << 20) / slot_bytes));
@@ -722,13 +811,29 @@ int pool_slot(Instance& I, uint32_t avail_mask, const int* avail, int dest, uint
 
 // Upload the table sets staged by pool_slot (one async copy through the ring
 // on the launch stream: no kernel reads a new slot before the copy, and no
-// in-flight kernel reads it at all -- slots are only rewritten after
-// pool_recycle's device-wide wait).  Then make `stream` wait for any table
-// copy still running on another stream.  Call before every launch that
-// reads the pool.
+// queued kernel reads it at all -- slots are only rewritten after the pool's
+// recycle, whose event a copy on another stream waits for).  Call before
+// every launch that reads the pool.
+//
+// pool_ev marks the last table copy.  A launch on another stream waits for
+// it; a copy on another stream first waits for the previous copy too, so
+// each new record covers every copy before it (a later launch that reads
+// slots of both copies waits for one event).  (Round-3 advisor: without that
+// wait, a stream reusing a pattern staged by another stream's still-running
+// copy could read its slot before the copy landed.)
 hipError_t pool_commit(Instance& I, hipStream_t stream) {
   hipError_t e = hipSuccess;
+  const bool other_pending = I.pool_ev_pending && I.pool_ev_stream != stream &&
+                             hipEventQuery(I.pool_ev) != hipSuccess;
+  if (I.pool_ev_pending && !other_pending && I.pool_ev_stream != stream) I.pool_ev_pending = false;
   if (!I.pool_stage.empty()) {
+    if (I.pool_gen_pending && I.pool_gen_stream != stream) {
+      if (hipEventQuery(I.pool_gen_ev) == hipSuccess)
+        I.pool_gen_pending = false;
+      else if ((e = hipStreamWaitEvent(stream, I.pool_gen_ev, 0)) != hipSuccess)
+        return e;
+    }
+    if (other_pending && (e = hipStreamWaitEvent(stream, I.pool_ev, 0)) != hipSuccess) return e;
     const size_t n = I.pool_stage.size();
     RingSlot* r = I.ring_acquire(n, &e);
     if (!r) return e;
@@ -747,12 +852,7 @@ hipError_t pool_commit(Instance& I, hipStream_t stream) {
     I.pool_ev_pending = true;
     return hipSuccess;
   }
-  if (I.pool_ev_pending && I.pool_ev_stream != stream) {
-    if (hipEventQuery(I.pool_ev) == hipSuccess)
-      I.pool_ev_pending = false;
-    else
-      e = hipStreamWaitEvent(stream, I.pool_ev, 0);
-  }
+  if (other_pending) e = hipStreamWaitEvent(stream, I.pool_ev, 0);
   return e;
 }
 
@@ -825,6 +925,7 @@ uint32_t passes_of(const DecodeJob& J, const DescBatch& B, int o0, int o1) {
 hipError_t launch_range(Instance& I, const DecodeJob& J, int o0, int o1, uint32_t passes,
                         const uint8_t* dev, uint64_t bs, hipStream_t stream) {
   const int n = o1 - o0;
+  if (hipError_t e = I.note_stream(stream); e != hipSuccess) return e;
   if (hipError_t e = pool_commit(I, stream); e != hipSuccess) return e;
   for (uint32_t p = 0; p < passes; ++p) {
     DecodeParams P{};
@@ -847,6 +948,7 @@ hipError_t launch_range(Instance& I, const DecodeJob& J, int o0, int o1, uint32_
     // passes == 1: every missing data row of every object is in this pass, so
     // the kernel stores all k data slices unconditionally (DecodeMode kDecode)
     P.mode = J.dest ? 1u : (passes == 1 ? 0u : 2u);
+    P.no_edge_blocks = I.knobs.edge_blocks ? 0u : 1u;
     hipError_t e = launch_decode(P, stream);
     if (e != hipSuccess) return e;
   }
@@ -873,12 +975,16 @@ int flush_range(Instance& I, const DecodeJob& J, const DescBatch& B, int o0, int
 // The kernels address an object's bytes and a stripe's fragments through
 // buffer descriptors with 32-bit offsets (ec_kernels_impl.hpp): j*bs + x for
 // object slices (decode's output descriptor holds 2^31 - 1 records, so that
-// voffset 2^31 drops a store), i*frag_stride + 80 + x inside a stripe
-// (2^32 - 1 records), and 32-bit item indices.  A layout past those limits
-// would wrap with no error, so it is refused before anything is launched.
-bool layout_fits(int k, int m, uint64_t bs, uint64_t frag_stride, uint64_t n_obj) {
+// voffset 2^31 drops a store; encode's input descriptor 2^32 - 1),
+// i*frag_stride + 80 + x inside a stripe (2^32 - 1 records), and 32-bit item
+// indices.  A layout past those limits would wrap with no error, so it is
+// refused (-EINVALIDPARAMS) before anything is launched: objects up to ~2 GiB
+// decode and ~4 GiB encode.
+bool layout_fits(int k, int m, uint64_t bs, uint64_t frag_stride, uint64_t n_obj,
+                 bool decode = true) {
   if (bs > 0xFFFFFFF0ull) return false;
-  if (static_cast<uint64_t>(k) * bs + 16 > 0x7FFFFFFFull) return false;
+  const uint64_t slice_limit = decode ? 0x7FFFFFFFull : 0xFFFFFFF0ull;
+  if (static_cast<uint64_t>(k) * bs + 16 > slice_limit) return false;
   if (static_cast<uint64_t>(k + m) * frag_stride > 0xFFFFFFF0ull) return false;
   return n_obj * (bs / 4096 + 1) < (1ull << 31);
 }
@@ -945,7 +1051,7 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
       if ((rc = flush_range(I, J, B, o0, o, bs, stream)) < 0) return rc;
       o0 = o;
       split = true;
-      pool_recycle(I);
+      if (const hipError_t er = pool_recycle(I, stream); er != hipSuccess) return hip_errno(er);
       rc = pool_slot(I, amask, avail, dest, &B.slots[o], B.outs[o]);
       if (rc == kPoolFull) return -ENOMEM;  // pool of zero slots
     }
@@ -974,16 +1080,18 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
   return e2 == hipSuccess ? 0 : hip_errno(e2);
 }
 
-// Device copy of per-payload-size CRC tables (a bounded cache: when full,
-// wait for its users, then drop it).  Returns null on failure (*err set).
+// Device copy of per-payload-size CRC tables (a bounded cache, ~9 KiB per
+// size: when full, wait for the instance's own launches -- its users -- then
+// drop it).  Returns null on failure (*err set).
+constexpr size_t kCrcTableSizes = 64;
 template <class T, class Build>
-const void* crc_table_cache(std::map<uint64_t, DevBuf>& cache, uint64_t bs, Build build,
-                            hipError_t* err) {
+const void* crc_table_cache(Instance& I, std::map<uint64_t, DevBuf>& cache, uint64_t bs,
+                            Build build, hipError_t* err) {
   *err = hipSuccess;
   auto it = cache.find(bs);
   if (it == cache.end()) {
-    if (cache.size() >= 16) {
-      (void)hipDeviceSynchronize();
+    if (cache.size() >= kCrcTableSizes) {
+      if ((*err = I.wait_streams()) != hipSuccess) return nullptr;
       for (auto& kv : cache) kv.second.release();
       cache.clear();
     }
@@ -1005,8 +1113,8 @@ const void* crc_table_cache(std::map<uint64_t, DevBuf>& cache, uint64_t bs, Buil
 const void* crc_tables_for(Instance& I, uint64_t bs, hipError_t* err) {
   const uint32_t steps = static_cast<uint32_t>((bs + 4095) / 4096);
   return crc_table_cache<CrcTables>(
-      I.crc_tables, bs, [&](CrcTables* t) { build_crc_tables(static_cast<uint32_t>(bs), steps, t); },
-      err);
+      I, I.crc_tables, bs,
+      [&](CrcTables* t) { build_crc_tables(static_cast<uint32_t>(bs), steps, t); }, err);
 }
 
 // Inline CRC-32 of `count` fragments per object (caller holds I.mu): payload
@@ -1028,7 +1136,8 @@ int run_crc(Instance& I, uint8_t* base, uint64_t frag_stride, uint64_t stripe_st
   P.bs = static_cast<uint32_t>(bs);
   P.steps = steps;
   P.tables = tables;
-  const hipError_t e = launch_crc(P, stream);
+  hipError_t e = I.note_stream(stream);
+  if (e == hipSuccess) e = launch_crc(P, stream);
   return e == hipSuccess ? 0 : hip_errno(e);
 }
 
@@ -1043,7 +1152,8 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
   if (n_obj > 1 && (obj_stride < obj_len || obj_stride % 16)) return -EINVALIDPARAMS;
   if (reinterpret_cast<uintptr_t>(parity) % 16 || reinterpret_cast<uintptr_t>(data) % 16)
     return -EINVALIDPARAMS;
-  if (!layout_fits(k, m, bs, frag_stride, static_cast<uint64_t>(n_obj))) return -EINVALIDPARAMS;
+  if (!layout_fits(k, m, bs, frag_stride, static_cast<uint64_t>(n_obj), false))
+    return -EINVALIDPARAMS;
   const size_t hdr_bytes = headers ? static_cast<size_t>(k + m) * kHeaderBytes : 0;
   Upload u;
   hipError_t e;
@@ -1064,19 +1174,22 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
     if (rc < 0) return rc;
   }
   // inline_crc32: the parity CRC fused into the encode launch
-  // (ECAMD_CRC_FUSED=0: the separate CRC pass, as for data fragments)
+  // (knob ECAMD_CRC_FUSED=0: the separate CRC pass, as for data fragments)
   const bool crc = headers && I.ct == CHKSUM_CRC32 && bs > 0;
-  const char* fused_env = std::getenv("ECAMD_CRC_FUSED");
-  const bool fused_crc = crc && !(fused_env && fused_env[0] == '0');
+  const bool fused_crc = crc && I.knobs.crc_fused;
   const void* crc_maps = nullptr;
   const void* crc_fin = nullptr;
   uint32_t* crc_part = nullptr;
+  if ((e = I.note_stream(stream)) != hipSuccess) {
+    (void)upload_done(I, u, stream);
+    return hip_errno(e);
+  }
   if (fused_crc) {
     const uint32_t total = static_cast<uint32_t>((bs + 4095) / 4096);
     hipError_t te;
     if (!(crc_maps = crc_tables_for(I, bs, &te)) ||
         !(crc_fin = crc_table_cache<CrcFinishTables>(
-              I.crc_finish, bs,
+              I, I.crc_finish, bs,
               [&](CrcFinishTables* t) { build_crc_finish_tables(static_cast<uint32_t>(bs), total, t); },
               &te))) {
       (void)upload_done(I, u, stream);
@@ -1088,7 +1201,10 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
       return hip_errno(e);
     }
   }
-  for (uint32_t p = 0; p < I.passes; ++p) {
+  // one eight-row pass for 4 < m <= 8 (the fused CRC keeps four-row passes)
+  const bool wide = I.wide && !fused_crc;
+  const uint32_t passes = wide ? 1 : I.passes;
+  for (uint32_t p = 0; p < passes; ++p) {
     EncodeParams P{};
     P.crc_tables = crc_maps;
     P.crc_finish_tables = crc_fin;
@@ -1100,15 +1216,17 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
     P.data = data;
     P.frag_stride = frag_stride;
     P.stripe_stride = stripe_stride;
-    P.tables = reinterpret_cast<const uint32_t*>(I.enc_tables.b() + p * I.table_bytes());
+    P.tables = wide ? reinterpret_cast<const uint32_t*>(I.enc_tables8.p)
+                    : reinterpret_cast<const uint32_t*>(I.enc_tables.b() + p * I.table_bytes());
     P.headers = u.dev;
     P.k = k;
     P.m = m;
     P.w = static_cast<uint32_t>(I.code.w);
     P.row0 = p * kRowsPerPass;
-    P.nrows = std::min<uint32_t>(kRowsPerPass, m - P.row0);
+    P.nrows = wide ? static_cast<uint32_t>(m) : std::min<uint32_t>(kRowsPerPass, m - P.row0);
     P.bs = static_cast<uint32_t>(bs);
     P.n_obj = n_obj;
+    P.no_edge_blocks = I.knobs.edge_blocks ? 0u : 1u;
     if (bs == 0) {
       // header-only fragments: nothing for the kernel to compute
       break;
@@ -1163,10 +1281,10 @@ int host_pipeline(Instance& I, int n_obj, const HostSide& H, Run run) {
   // (tools/host_ab.py, k=10 m=4, 256 x 4 MiB): encode 50.4 GiB/s, decode
   // 40.5, against 39.7 / 27.4 for the copy-engine pipeline below (whose
   // H2D and D2H copies, run together, reach only 36 GiB/s each way).
-  // ECAMD_HOST_STAGED=1 forces the copy-engine pipeline.
+  // Knob ECAMD_HOST_STAGED=1 forces the copy-engine pipeline.
   const uint64_t in_total = static_cast<uint64_t>(n_obj - 1) * H.in_stride + H.in_last;
   const uint64_t out_total = static_cast<uint64_t>(n_obj - 1) * H.out_stride + H.out_last;
-  if (!env_on("ECAMD_HOST_STAGED") && device_mapped(H.in, in_total) &&
+  if (!I.knobs.host_staged && device_mapped(H.in, in_total) &&
       device_mapped(H.out, out_total)) {
     if (!I.hstream[0]) {
       hipError_t e = hipStreamCreateWithFlags(&I.hstream[0], hipStreamNonBlocking);
@@ -1182,12 +1300,12 @@ int host_pipeline(Instance& I, int n_obj, const HostSide& H, Run run) {
   // chunks' inputs H2D; ECAMD_HOST_STAGED_OUT=1 stages outputs through HBM +
   // D2H copies instead (measured round 2: 44.8 / 30.4 GiB/s vs 39.7 / 27.4
   // direct-out, both below the direct path above).
-  const bool out_direct = !env_on("ECAMD_HOST_STAGED_OUT") && device_mapped(H.out, out_total);
+  const bool out_direct = !I.knobs.host_staged_out && device_mapped(H.out, out_total);
   // ~32 MiB of input per chunk, at least 2 chunks per stream when the batch
   // allows, so the three stages overlap for most of the batch.
-  // ECAMD_HOST_CHUNK_MB / ECAMD_HOST_STREAMS: tuning knobs (tools/host_ab.py).
-  const int nstreams = std::max(1, std::min(kHostStreams, env_int("ECAMD_HOST_STREAMS", 3)));
-  const uint64_t chunk_bytes = static_cast<uint64_t>(std::max(1, env_int("ECAMD_HOST_CHUNK_MB", 32))) << 20;
+  // Knobs ECAMD_HOST_CHUNK_MB / ECAMD_HOST_STREAMS: tuning (tools/host_ab.py).
+  const int nstreams = std::max(1, std::min(kHostStreams, I.knobs.host_streams));
+  const uint64_t chunk_bytes = static_cast<uint64_t>(I.knobs.host_chunk_mb) << 20;
   int chunk = static_cast<int>(std::max<uint64_t>(1, chunk_bytes / H.in_stride));
   chunk = std::min(chunk, std::max(1, (n_obj + 2 * nstreams - 1) / (2 * nstreams)));
   const uint64_t in_cap = (static_cast<uint64_t>(chunk) * H.in_stride + H.in_skew + 255) & ~255ull;
@@ -1264,6 +1382,7 @@ int liberasurecode_instance_create(const ec_backend_id_t id, struct ec_args* arg
   I->backend_id = id;
   I->code = *code;
   I->legacy_crc = write_legacy_crc();
+  I->knobs = Knobs::from_env();
   I->passes = (I->m + kRowsPerPass - 1) / kRowsPerPass;
   if (hipGetDevice(&I->device) != hipSuccess) return -EBACKENDNOTAVAIL;
   I->gen = id == EC_BACKEND_ISA_L_RS_CAUCHY ? make_isal_cauchy_matrix(I->k, I->m)
@@ -1285,6 +1404,15 @@ int liberasurecode_instance_create(const ec_backend_id_t id, struct ec_args* arg
     if (e == hipSuccess)
       e = hipMemcpy(I->enc_tables.p, host.data(), host.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) return hip_errno(e);
+    I->wide = I->code.w == 16 && I->m > kRowsPerPass && I->m <= kRowsWide;
+    if (I->wide) {
+      std::vector<uint16_t> t8(static_cast<size_t>(I->k) * 4 * 16 * kRowsWide, 0);
+      build_nibble_tables_x8(&I->gen[static_cast<size_t>(I->k) * I->k], I->m, I->k, t8.data());
+      const size_t bytes = t8.size() * sizeof(uint16_t);
+      e = I->enc_tables8.ensure(bytes);
+      if (e == hipSuccess) e = hipMemcpy(I->enc_tables8.p, t8.data(), bytes, hipMemcpyHostToDevice);
+      if (e != hipSuccess) return hip_errno(e);
+    }
   }
   args->w = I->code.w;
   std::lock_guard<std::mutex> lk(g_registry_mu);
@@ -1305,6 +1433,99 @@ int liberasurecode_instance_destroy(int desc) {
   std::lock_guard<std::mutex> lk(I->mu);  // wait for in-flight calls
   return 0;
 }
+
+namespace {
+
+// liberasurecode_encode's work for one object, into k + m caller-provided
+// fragments of bs + 80 bytes (caller holds I.mu, device set).  The object is
+// copied into pinned, device-mapped staging (host_copy: parallel for large
+// objects) and the kernel reads it there over PCIe; while it runs, the host
+// fills the data fragments from the caller's object (prepare_fragments_for_
+// encode's copy), then copies the parity out.  Objects past the
+// single_pinned_max knob take DMA copies through HBM instead.
+// Phase clock of the single-object calls (Instance::phase_us).
+struct PhaseClock {
+  double* out;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  explicit PhaseClock(double* o) : out(o) {
+    for (int i = 0; i < 6; ++i) out[i] = 0;
+  }
+  void mark(int phase) {
+    const auto now = std::chrono::steady_clock::now();
+    out[phase] += std::chrono::duration<double, std::micro>(now - t).count();
+    t = now;
+  }
+};
+
+int encode_into(Instance& I, const char* data, uint64_t len, uint8_t* const* frags) {
+  const int k = I.k, m = I.m;
+  PhaseClock clk(I.phase_us);
+  const uint64_t bs = blocksize_of(k, I.code.w, len);
+  thread_local std::vector<CopyJob> jobs;
+  auto data_fragments = [&] {  // payloads = the object's slices, zero padded
+    jobs.clear();
+    uint64_t left = len;
+    const char* src = data;
+    for (int j = 0; j < k; ++j) {
+      const uint64_t c = std::min(left, bs);
+      if (c) jobs.push_back({frags[j] + kHeaderBytes, src, c});
+      if (c < bs) jobs.push_back({frags[j] + kHeaderBytes + c, nullptr, bs - c});
+      src += c;
+      left -= c;
+    }
+    host_copy(jobs.data(), static_cast<int>(jobs.size()));
+  };
+  if (bs > 0) {
+    const uint64_t fs = round16(kHeaderBytes + round16(bs));
+    const uint64_t obj_bytes = round16(len);
+    uint8_t* pin = len <= I.knobs.single_pinned_max ? I.pin.ensure(obj_bytes + fs * m) : nullptr;
+    hipError_t e = hipSuccess;
+    if (!pin && (e = I.scratch.ensure(obj_bytes + fs * m)) != hipSuccess) return hip_errno(e);
+    uint8_t* d_obj = pin ? pin : I.scratch.b();
+    uint8_t* d_par = d_obj + obj_bytes;
+    if (pin) {
+      const CopyJob in[2] = {{d_obj, data, len}, {d_obj + len, nullptr, obj_bytes - len}};
+      host_copy(in, 2);
+    } else if ((e = hipMemcpyAsync(d_obj, data, len, hipMemcpyHostToDevice, I.stream)) !=
+               hipSuccess) {
+      return hip_errno(e);
+    }
+    clk.mark(0);
+    int rc = run_encode(I, d_obj, obj_bytes, len, 1, d_par, nullptr, fs, fs * m, false, I.stream);
+    if (rc < 0) {
+      (void)hipStreamSynchronize(I.stream);
+      return rc;
+    }
+    clk.mark(1);
+    data_fragments();  // on the host, beside the kernel
+    clk.mark(2);
+    if (!pin)
+      for (int p = 0; p < m; ++p)
+        if ((e = hipMemcpyAsync(frags[k + p] + kHeaderBytes, d_par + p * fs + kHeaderBytes, bs,
+                                hipMemcpyDeviceToHost, I.stream)) != hipSuccess) {
+          (void)hipStreamSynchronize(I.stream);
+          return hip_errno(e);
+        }
+    if ((e = hipStreamSynchronize(I.stream)) != hipSuccess) return hip_errno(e);
+    clk.mark(3);
+    if (pin) {
+      jobs.clear();
+      for (int p = 0; p < m; ++p)
+        jobs.push_back({frags[k + p] + kHeaderBytes, d_par + p * fs + kHeaderBytes, bs});
+      host_copy(jobs.data(), static_cast<int>(jobs.size()));
+    }
+    clk.mark(4);
+  } else {
+    data_fragments();
+  }
+  for (int i = 0; i < k + m; ++i)
+    make_header(frags[i], I.code, i, static_cast<uint32_t>(bs), len, I.ct,
+                frags[i] + kHeaderBytes, I.legacy_crc);
+  clk.mark(5);
+  return 0;
+}
+
+}  // namespace
 
 int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_size,
                           char*** encoded_data, char*** encoded_parity, uint64_t* fragment_len) {
@@ -1328,54 +1549,17 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
     return rc;
   };
   if (!dat || !par) return fail(-ENOMEM);
-  uint64_t left = orig_data_size;
-  const char* src = orig_data;
+  uint8_t* frags[kMaxFragments];
   for (int j = 0; j < k; ++j) {
-    if (!(dat[j] = alloc_fragment(fl))) return fail(-ENOMEM);
-    const uint64_t c = std::min(left, bs);
-    if (c) std::memcpy(dat[j] + kHeaderBytes, src, c);
-    src += c;
-    left -= c;
+    if (!(dat[j] = alloc_fragment(fl, false))) return fail(-ENOMEM);
+    frags[j] = reinterpret_cast<uint8_t*>(dat[j]);
   }
-  for (int p = 0; p < m; ++p)
-    if (!(par[p] = alloc_fragment(fl))) return fail(-ENOMEM);
-
-  if (bs > 0) {
-    const uint64_t fs = round16(kHeaderBytes + round16(bs));
-    const uint64_t obj_bytes = round16(orig_data_size);
-    uint8_t* pin = orig_data_size <= single_pinned_max() ? I->pin.ensure(obj_bytes + fs * m)
-                                                         : nullptr;
-    hipError_t e = hipSuccess;
-    if (!pin && (e = I->scratch.ensure(obj_bytes + fs * m)) != hipSuccess)
-      return fail(hip_errno(e));
-    uint8_t* d_obj = pin ? pin : I->scratch.b();
-    uint8_t* d_par = d_obj + obj_bytes;
-    if (pin)
-      std::memcpy(d_obj, orig_data, orig_data_size);
-    else if ((e = hipMemcpyAsync(d_obj, orig_data, orig_data_size, hipMemcpyHostToDevice,
-                                 I->stream)) != hipSuccess)
-      return fail(hip_errno(e));
-    int rc = run_encode(*I, d_obj, obj_bytes, orig_data_size, 1, d_par, nullptr, fs, fs * m,
-                        false, I->stream);
-    if (rc < 0) return fail(rc);
-    if (!pin)
-      for (int p = 0; p < m; ++p)
-        if ((e = hipMemcpyAsync(par[p] + kHeaderBytes, d_par + p * fs + kHeaderBytes, bs,
-                                hipMemcpyDeviceToHost, I->stream)) != hipSuccess)
-          return fail(hip_errno(e));
-    if ((e = hipStreamSynchronize(I->stream)) != hipSuccess) return fail(hip_errno(e));
-    if (pin)
-      for (int p = 0; p < m; ++p)
-        std::memcpy(par[p] + kHeaderBytes, d_par + p * fs + kHeaderBytes, bs);
+  for (int p = 0; p < m; ++p) {
+    if (!(par[p] = alloc_fragment(fl, false))) return fail(-ENOMEM);
+    frags[k + p] = reinterpret_cast<uint8_t*>(par[p]);
   }
-  for (int j = 0; j < k; ++j)
-    make_header(reinterpret_cast<uint8_t*>(dat[j]), I->code, j, static_cast<uint32_t>(bs),
-                orig_data_size, I->ct, reinterpret_cast<uint8_t*>(dat[j]) + kHeaderBytes,
-                I->legacy_crc);
-  for (int p = 0; p < m; ++p)
-    make_header(reinterpret_cast<uint8_t*>(par[p]), I->code, k + p, static_cast<uint32_t>(bs),
-                orig_data_size, I->ct, reinterpret_cast<uint8_t*>(par[p]) + kHeaderBytes,
-                I->legacy_crc);
+  const int rc = encode_into(*I, orig_data, orig_data_size, frags);
+  if (rc < 0) return fail(rc);
   *encoded_data = dat;
   *encoded_parity = par;
   *fragment_len = fl;
@@ -1439,26 +1623,117 @@ int partition(const Instance& I, char** frags, int n, Partition& P) {
 }
 
 // Upload the first k available payloads into a [k+m][fs] device image.
-// (`pinned`: d_frags is the zero-copy staging buffer, filled with memcpy.)
+// (`pinned`: d_frags is the zero-copy staging buffer, filled on the host.)
 int stage_fragments(Instance& I, const Partition& P, uint64_t bs, uint64_t fs, uint8_t* d_frags,
                     uint32_t* mask, bool pinned) {
   int c = 0;
   *mask = 0;
+  thread_local std::vector<CopyJob> jobs;
+  jobs.clear();
   for (int i = 0; i < I.k + I.m && c < I.k; ++i) {
     if (!P.by_idx[i]) continue;
     if (pinned) {
-      std::memcpy(d_frags + i * fs + kHeaderBytes, P.by_idx[i] + kHeaderBytes, bs);
-      *mask |= 1u << i;
-      ++c;
-      continue;
+      jobs.push_back({d_frags + i * fs + kHeaderBytes, P.by_idx[i] + kHeaderBytes, bs});
+    } else {
+      hipError_t e = hipMemcpyAsync(d_frags + i * fs + kHeaderBytes, P.by_idx[i] + kHeaderBytes,
+                                    bs, hipMemcpyHostToDevice, I.stream);
+      if (e != hipSuccess) return hip_errno(e);
     }
-    hipError_t e = hipMemcpyAsync(d_frags + i * fs + kHeaderBytes, P.by_idx[i] + kHeaderBytes, bs,
-                                  hipMemcpyHostToDevice, I.stream);
-    if (e != hipSuccess) return hip_errno(e);
     *mask |= 1u << i;
     ++c;
   }
+  if (pinned) host_copy(jobs.data(), static_cast<int>(jobs.size()));
   return c == I.k ? 0 : -EINSUFFFRAGS;
+}
+
+// liberasurecode_decode's checks and partition (caller holds I.mu): the
+// decoded length and the fragments by index, or -errno.
+struct DecodeIn {
+  Partition P;
+  int part_rc = 0;  // partition()'s result (-EINSUFFFRAGS / -EBADHEADER) for the GF path
+  bool all_data = true;
+  uint64_t orig = 0, bs = 0;
+};
+
+int decode_prepare(Instance& I, char** frags, int n, uint64_t fragment_len, int force_checks,
+                   DecodeIn& D) {
+  const int k = I.k;
+  if (n < k) return -EINSUFFFRAGS;
+  if (fragment_len < kHeaderBytes) return -EBADHEADER;
+  for (int i = 0; i < n; ++i)
+    if (!frags[i] || header_invalid(reinterpret_cast<const uint8_t*>(frags[i]))) return -EBADHEADER;
+  if (force_checks) {
+    int bad = 0;
+    for (int i = 0; i < n; ++i)
+      bad += fragment_invalid(reinterpret_cast<const uint8_t*>(frags[i]), I.code.wire_id);
+    if (n - bad < k) return -EINSUFFFRAGS;
+  }
+  // fragments_to_string preconditions: consistent orig_data_size, and every
+  // payload size field inside the fragment buffer (a corrupt or crafted size
+  // must not make the copies below read past it)
+  D.orig = get64(frags[0] + 12);
+  for (int i = 0; i < n; ++i) {
+    if (get64(frags[i] + 12) != D.orig) return -EBADHEADER;
+    if (static_cast<uint64_t>(get32(frags[i] + 4)) + kHeaderBytes > fragment_len) return -EBADHEADER;
+  }
+  D.part_rc = partition(I, frags, n, D.P);
+  D.all_data = true;
+  for (int j = 0; j < k; ++j) D.all_data &= D.P.by_idx[j] != nullptr;
+  D.bs = 0;
+  for (int i = 0; i < k + I.m; ++i)
+    if (D.P.by_idx[i]) {
+      D.bs = get32(D.P.by_idx[i] + 4);
+      break;
+    }
+  if (D.bs + kHeaderBytes > fragment_len) return -EBADHEADER;
+  if (!(D.all_data && D.part_rc != -EBADHEADER) && D.part_rc < 0) return D.part_rc;
+  return 0;
+}
+
+// Decode into `out` (D.orig bytes; caller holds I.mu, device set).
+int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
+  const int k = I.k;
+  PhaseClock clk(I.phase_us);
+  const uint64_t orig = D.orig, bs = D.bs;
+  if (D.all_data && D.part_rc != -EBADHEADER) {
+    // Fast path (fragments_to_string): every data fragment present, no GF work.
+    thread_local std::vector<CopyJob> jobs;
+    jobs.clear();
+    uint64_t off = 0;
+    for (int j = 0; j < k && off < orig; ++j) {
+      const uint64_t c = std::min<uint64_t>(orig - off, get32(D.P.by_idx[j] + 4));
+      jobs.push_back({out + off, D.P.by_idx[j] + kHeaderBytes, c});
+      off += c;
+    }
+    if (off < orig) jobs.push_back({out + off, nullptr, orig - off});  // short size fields
+    host_copy(jobs.data(), static_cast<int>(jobs.size()));
+    clk.mark(4);
+    return 0;
+  }
+  const uint64_t fs = round16(kHeaderBytes + round16(bs));
+  const uint64_t obj_bytes = round16(orig);
+  const size_t need = fs * (k + I.m) + obj_bytes;
+  uint8_t* pin = orig <= I.knobs.single_pinned_max ? I.pin.ensure(need) : nullptr;
+  hipError_t e = hipSuccess;
+  if (!pin && (e = I.scratch.ensure(need)) != hipSuccess) return hip_errno(e);
+  uint8_t* d_frags = pin ? pin : I.scratch.b();
+  uint8_t* d_obj = d_frags + fs * (k + I.m);
+  uint32_t mask = 0;
+  int rc = stage_fragments(I, D.P, bs, fs, d_frags, &mask, pin != nullptr);
+  clk.mark(0);
+  if (rc == 0) {
+    DecodeJob J{d_frags, fs, fs * (k + I.m), orig, d_obj, obj_bytes, 1, &mask, nullptr, nullptr};
+    rc = run_decode(I, J, I.stream);
+  }
+  if (rc == 0 && orig && !pin)
+    if ((e = hipMemcpyAsync(out, d_obj, orig, hipMemcpyDeviceToHost, I.stream)) != hipSuccess)
+      rc = hip_errno(e);
+  clk.mark(1);
+  if ((e = hipStreamSynchronize(I.stream)) != hipSuccess && rc == 0) rc = hip_errno(e);
+  clk.mark(3);
+  if (rc == 0 && orig && pin) host_copy(out, d_obj, orig);
+  clk.mark(4);
+  return rc;
 }
 
 }  // namespace
@@ -1471,87 +1746,18 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
   if (!I) return -EBACKENDNOTAVAIL;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
-  const int k = I->k;
-  if (num_fragments < k) return -EINSUFFFRAGS;
-  if (fragment_len < kHeaderBytes) return -EBADHEADER;
-  for (int i = 0; i < num_fragments; ++i)
-    if (!available_fragments[i] ||
-        header_invalid(reinterpret_cast<const uint8_t*>(available_fragments[i])))
-      return -EBADHEADER;
-  if (force_metadata_checks) {
-    int bad = 0;
-    for (int i = 0; i < num_fragments; ++i)
-      bad += fragment_invalid(reinterpret_cast<const uint8_t*>(available_fragments[i]),
-                              I->code.wire_id);
-    if (num_fragments - bad < k) return -EINSUFFFRAGS;
-  }
-  // fragments_to_string preconditions: consistent orig_data_size, and every
-  // payload size field inside the fragment buffer (a corrupt or crafted size
-  // must not make the copies below read past it)
-  const uint64_t orig = get64(available_fragments[0] + 12);
-  for (int i = 0; i < num_fragments; ++i) {
-    if (get64(available_fragments[i] + 12) != orig) return -EBADHEADER;
-    if (static_cast<uint64_t>(get32(available_fragments[i] + 4)) + kHeaderBytes > fragment_len)
-      return -EBADHEADER;
-  }
-  Partition P;
-  int rc = partition(*I, available_fragments, num_fragments, P);
-  bool all_data = true;
-  for (int j = 0; j < k; ++j) all_data &= P.by_idx[j] != nullptr;
-  uint64_t bs = 0;
-  for (int i = 0; i < k + I->m; ++i)
-    if (P.by_idx[i]) {
-      bs = get32(P.by_idx[i] + 4);
-      break;
-    }
-  if (bs + kHeaderBytes > fragment_len) return -EBADHEADER;
-  char* out = static_cast<char*>(alloc_fragment(orig, false));
+  DecodeIn D;
+  int rc = decode_prepare(*I, available_fragments, num_fragments, fragment_len,
+                          force_metadata_checks, D);
+  if (rc < 0) return rc;
+  char* out = static_cast<char*>(alloc_fragment(D.orig, false));
   if (!out) return -ENOMEM;
-  if (all_data && rc != -EBADHEADER) {
-    // Fast path (fragments_to_string): every data fragment present, no GF work.
-    uint64_t off = 0;
-    for (int j = 0; j < k && off < orig; ++j) {
-      const uint64_t c = std::min<uint64_t>(orig - off, get32(P.by_idx[j] + 4));
-      std::memcpy(out + off, P.by_idx[j] + kHeaderBytes, c);
-      off += c;
-    }
-    if (off < orig) std::memset(out + off, 0, orig - off);  // short size fields
-    *out_data = out;
-    *out_data_len = orig;
-    return 0;
-  }
-  if (rc < 0) {
-    std::free(out);
-    return rc;
-  }
-  const uint64_t fs = round16(kHeaderBytes + round16(bs));
-  const uint64_t obj_bytes = round16(orig);
-  const size_t need = fs * (k + I->m) + obj_bytes;
-  uint8_t* pin = orig <= single_pinned_max() ? I->pin.ensure(need) : nullptr;
-  hipError_t e = hipSuccess;
-  if (!pin && (e = I->scratch.ensure(need)) != hipSuccess) {
-    std::free(out);
-    return hip_errno(e);
-  }
-  uint8_t* d_frags = pin ? pin : I->scratch.b();
-  uint8_t* d_obj = d_frags + fs * (k + I->m);
-  uint32_t mask = 0;
-  rc = stage_fragments(*I, P, bs, fs, d_frags, &mask, pin != nullptr);
-  if (rc == 0) {
-    DecodeJob J{d_frags, fs, fs * (k + I->m), orig, d_obj, obj_bytes, 1, &mask, nullptr, nullptr};
-    rc = run_decode(*I, J, I->stream);
-  }
-  if (rc == 0 && orig && !pin)
-    if ((e = hipMemcpyAsync(out, d_obj, orig, hipMemcpyDeviceToHost, I->stream)) != hipSuccess)
-      rc = hip_errno(e);
-  if ((e = hipStreamSynchronize(I->stream)) != hipSuccess && rc == 0) rc = hip_errno(e);
-  if (rc == 0 && orig && pin) std::memcpy(out, d_obj, orig);
-  if (rc < 0) {
+  if ((rc = decode_into(*I, D, reinterpret_cast<uint8_t*>(out))) < 0) {
     std::free(out);
     return rc;
   }
   *out_data = out;
-  *out_data_len = orig;
+  *out_data_len = D.orig;
   return 0;
 }
 
@@ -1593,7 +1799,7 @@ int liberasurecode_reconstruct_fragment(int desc, char** available_fragments, in
   if (bs > 0) {
     const uint64_t fs = round16(kHeaderBytes + round16(bs));
     const size_t need = fs * (k + m + 1);
-    uint8_t* pin = orig <= single_pinned_max() ? I->pin.ensure(need) : nullptr;
+    uint8_t* pin = orig <= I->knobs.single_pinned_max ? I->pin.ensure(need) : nullptr;
     hipError_t e = hipSuccess;
     if (!pin && (e = I->scratch.ensure(need)) != hipSuccess) return hip_errno(e);
     uint8_t* d_frags = pin ? pin : I->scratch.b();
@@ -1684,6 +1890,49 @@ int liberasurecode_get_fragment_size(int desc, int data_len) {
 uint32_t liberasurecode_get_version(void) { return kLibecVersion; }
 
 /* ---------------- Part 2 ---------------- */
+
+int ecamd_call_phases(int desc, double* us, int n) {
+  auto I = lookup(desc);
+  if (!I) return -EBACKENDNOTAVAIL;
+  if (!us || n < 0) return -EINVALIDPARAMS;
+  std::lock_guard<std::mutex> lk(I->mu);
+  const int c = std::min(n, 6);
+  for (int i = 0; i < c; ++i) us[i] = I->phase_us[i];
+  return c;
+}
+
+int ecamd_encode_into(int desc, const char* data, uint64_t data_len, char** fragments,
+                      uint64_t fragment_len) {
+  if (!data || !fragments) return -EINVALIDPARAMS;
+  auto I = lookup(desc);
+  if (!I) return -EBACKENDNOTAVAIL;
+  std::lock_guard<std::mutex> lk(I->mu);
+  DeviceGuard g(I->device);
+  if (fragment_len != blocksize_of(I->k, I->code.w, data_len) + kHeaderBytes)
+    return -EINVALIDPARAMS;
+  uint8_t* frags[kMaxFragments];
+  for (int i = 0; i < I->k + I->m; ++i) {
+    if (!fragments[i]) return -EINVALIDPARAMS;
+    frags[i] = reinterpret_cast<uint8_t*>(fragments[i]);
+  }
+  return encode_into(*I, data, data_len, frags);
+}
+
+int ecamd_decode_into(int desc, char** available_fragments, int num_fragments,
+                      uint64_t fragment_len, int force_metadata_checks, char* out,
+                      uint64_t out_len) {
+  if (!available_fragments || (!out && out_len)) return -EINVALIDPARAMS;
+  auto I = lookup(desc);
+  if (!I) return -EBACKENDNOTAVAIL;
+  std::lock_guard<std::mutex> lk(I->mu);
+  DeviceGuard g(I->device);
+  DecodeIn D;
+  const int rc = decode_prepare(*I, available_fragments, num_fragments, fragment_len,
+                                force_metadata_checks, D);
+  if (rc < 0) return rc;
+  if (out_len != D.orig) return -EINVALIDPARAMS;
+  return decode_into(*I, D, reinterpret_cast<uint8_t*>(out));
+}
 
 uint64_t ecamd_blocksize(int desc, uint64_t obj_len) {
   auto I = lookup(desc);

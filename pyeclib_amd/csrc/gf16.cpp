@@ -93,4 +93,22 @@ void build_nibble_tables(const uint16_t* rows, int nrows, int ncols, uint64_t* o
     }
 }
 
+void build_nibble_tables_x8(const uint16_t* rows, int nrows, int ncols, uint16_t* out) {
+  const Gf16& gf = Gf16::get();
+  for (int c = 0; c < ncols; ++c)
+    for (int q = 0; q < 4; ++q) {
+      uint16_t basis[4][kRowsWide] = {};
+      for (int b = 0; b < 4; ++b) {
+        const uint16_t x = static_cast<uint16_t>(1u << (4 * q + b));
+        for (int r = 0; r < nrows && r < kRowsWide; ++r) basis[b][r] = gf.mul(rows[r * ncols + c], x);
+      }
+      uint16_t* t = out + (c * 4 + q) * 16 * kRowsWide;
+      for (int v = 0; v < 16; ++v)
+        for (int r = 0; r < kRowsWide; ++r)
+          t[v * kRowsWide + r] = static_cast<uint16_t>(
+              ((v & 1) ? basis[0][r] : 0) ^ ((v & 2) ? basis[1][r] : 0) ^
+              ((v & 4) ? basis[2][r] : 0) ^ ((v & 8) ? basis[3][r] : 0));
+    }
+}
+
 }  // namespace ecamd

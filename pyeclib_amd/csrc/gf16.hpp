@@ -64,4 +64,13 @@ bool invert(const GfMatrix& a, GfMatrix& out, int n);
 // compile-time offset (ec_kernels_impl.hpp).  One table set is C * 512 B.
 void build_nibble_tables(const uint16_t* rows, int nrows, int ncols, uint64_t* out);
 
+// Eight-row tables (4 < R <= 8: one encode pass for m = 5..8 instead of two
+// passes that each re-read the object).  Entry (c, q, v) is 16 bytes: the
+// eight 16-bit products M[r][c] * (v << 4q), r = 0..7 (zero for r >= R), at
+// bytes 2r..2r+1.  Layout [c][q][v]: entry at byte 1024c + 256q + 16v, so the
+// lookup address is again the nibble times 16 plus a compile-time offset,
+// read with one ds_read_b128 per nibble.  One table set is C * 1024 B.
+constexpr int kRowsWide = 8;
+void build_nibble_tables_x8(const uint16_t* rows, int nrows, int ncols, uint16_t* out);
+
 }  // namespace ecamd

@@ -1,0 +1,135 @@
+#include "host_copy.hpp"
+
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace ecamd {
+namespace {
+
+constexpr size_t kParallelMin = 256 << 10;  // smaller copies stay on the caller
+constexpr size_t kPiece = 64 << 10;
+
+struct Piece {
+  uint8_t* dst;
+  const uint8_t* src;
+  size_t n;
+};
+
+void run_piece(const Piece& p) {
+  if (p.src)
+    std::memcpy(p.dst, p.src, p.n);
+  else
+    std::memset(p.dst, 0, p.n);
+}
+
+class Pool {
+ public:
+  explicit Pool(int threads) : pid_(getpid()) {
+    for (int i = 0; i < threads; ++i) threads_.emplace_back([this] { work(); });
+  }
+  // the pool lives for the process (threads detached at exit: no join at
+  // static destruction, which may run after the runtime is gone)
+  ~Pool() {
+    for (auto& t : threads_) t.detach();
+  }
+  bool usable() const { return !threads_.empty() && getpid() == pid_; }
+
+  void run(const std::vector<Piece>& pieces) {
+    std::lock_guard<std::mutex> one(submit_mu_);  // one batch at a time
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      batch_ = &pieces;
+      next_.store(0);
+      done_.store(0);
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain(pieces);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return done_.load() == pieces.size() && busy_ == 0; });
+    batch_ = nullptr;
+  }
+
+ private:
+  void drain(const std::vector<Piece>& pieces) {
+    size_t i;
+    while ((i = next_.fetch_add(1)) < pieces.size()) {
+      run_piece(pieces[i]);
+      if (done_.fetch_add(1) + 1 == pieces.size()) {
+        std::lock_guard<std::mutex> lk(mu_);
+        done_cv_.notify_all();
+      }
+    }
+  }
+  void work() {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::vector<Piece>* b;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen && batch_ != nullptr; });
+        seen = gen_;
+        b = batch_;
+        ++busy_;
+      }
+      drain(*b);
+      std::lock_guard<std::mutex> lk(mu_);
+      --busy_;
+      done_cv_.notify_all();
+    }
+  }
+
+  pid_t pid_;
+  std::vector<std::thread> threads_;
+  std::mutex submit_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::vector<Piece>* batch_ = nullptr;
+  uint64_t gen_ = 0;
+  int busy_ = 0;
+  std::atomic<size_t> next_{0}, done_{0};
+};
+
+int threads_from_env() {
+  const char* v = std::getenv("ECAMD_COPY_THREADS");
+  const int n = (v == nullptr || *v == 0) ? 4 : std::atoi(v);
+  return std::max(0, std::min(n, 32));
+}
+
+Pool& pool() {
+  static Pool* p = new Pool(threads_from_env());  // never destroyed: see ~Pool
+  return *p;
+}
+
+}  // namespace
+
+int host_copy_threads() { return threads_from_env(); }
+
+void host_copy(const CopyJob* jobs, int count) {
+  size_t total = 0;
+  for (int i = 0; i < count; ++i) total += jobs[i].n;
+  if (total < kParallelMin || !pool().usable()) {
+    for (int i = 0; i < count; ++i)
+      run_piece({static_cast<uint8_t*>(jobs[i].dst), static_cast<const uint8_t*>(jobs[i].src),
+                 jobs[i].n});
+    return;
+  }
+  thread_local std::vector<Piece> pieces;
+  pieces.clear();
+  for (int i = 0; i < count; ++i) {
+    auto* d = static_cast<uint8_t*>(jobs[i].dst);
+    auto* s = static_cast<const uint8_t*>(jobs[i].src);
+    for (size_t off = 0; off < jobs[i].n; off += kPiece)
+      pieces.push_back({d + off, s ? s + off : nullptr, std::min(kPiece, jobs[i].n - off)});
+  }
+  pool().run(pieces);
+}
+
+}  // namespace ecamd

@@ -315,3 +315,36 @@ def test_single_object_staging_paths(oracle, monkeypatch, pinned_max, n):
     assert drv.reconstruct(frags[1:k + 1], [0])[0] == frags[0]
     assert drv.reconstruct(frags[:k], [k + 2])[0] == frags[k + 2]
     drv.close()
+
+
+@pytest.mark.parametrize("n", [1, 4093, (1 << 20) + 5, (4 << 20) + 17])
+def test_liberasurecode_entry_points_match_into_forms(oracle, n):
+    """The entry points pyeclib_c.c binds (liberasurecode_encode / _decode /
+    _cleanup, pyeclib_c.c:537, :562, :878, :919) called through ctypes, as
+    the reference binding calls them: the same fragments as the oracle and as
+    the ecamd_*_into forms the Python binding uses, and the same decoded bytes."""
+    import ctypes
+    P = ctypes.POINTER
+    k, m = 10, 4
+    drv = ECDriver(k=k, m=m, ec_type="liberasurecode_rs_vand")
+    desc = drv.ec_lib_reference.handle.desc
+    data = os.urandom(n)
+    dat, par = P(ctypes.c_void_p)(), P(ctypes.c_void_p)()
+    flen = ctypes.c_uint64(0)
+    assert _native.lib.liberasurecode_encode(desc, data, n, ctypes.byref(dat), ctypes.byref(par),
+                                             ctypes.byref(flen)) == 0
+    fl = flen.value
+    frags = [ctypes.string_at(dat[i], fl) for i in range(k)] + \
+            [ctypes.string_at(par[i], fl) for i in range(m)]
+    assert _native.lib.liberasurecode_encode_cleanup(desc, dat, par) == 0
+    assert frags == oracle.encode(k, m, data)
+    assert drv.encode(data) == frags  # ecamd_encode_into
+    for avail in (frags[m:m + k], frags[:k]):  # GPU path, concatenation fast path
+        arr = (ctypes.c_char_p * k)(*avail)
+        out, olen = ctypes.c_void_p(), ctypes.c_uint64(0)
+        assert _native.lib.liberasurecode_decode(desc, arr, k, fl, 0, ctypes.byref(out),
+                                                 ctypes.byref(olen)) == 0
+        assert olen.value == n and ctypes.string_at(out.value, n) == data
+        assert _native.lib.liberasurecode_decode_cleanup(desc, out) == 0
+        assert drv.decode(avail) == data  # ecamd_decode_into
+    drv.close()

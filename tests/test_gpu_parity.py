@@ -12,8 +12,9 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
+# m = 5..8 (rs_vand): one eight-row encode pass (Gf16x8); m = 9: four-row passes
 CONFIGS = [(4, 2), (10, 4), (12, 2), (11, 2), (10, 2), (8, 4), (12, 4), (3, 5), (6, 9), (20, 4),
-           (1, 1), (2, 1), (28, 4)]
+           (1, 1), (2, 1), (28, 4), (10, 5), (12, 6), (8, 8), (7, 7), (24, 8)]
 LENGTHS = [1, 2, 9, 31, 100, 1000, 4099, 8192, 65536 + 3, 262144, 1 << 20]
 
 
@@ -39,7 +40,8 @@ def test_encode_matches_oracle(amd, oracle, k, m):
             assert g == w, f"k={k} m={m} len={n} fragment {idx} differs"
 
 
-@pytest.mark.parametrize("k,m", [(4, 2), (10, 4), (12, 2), (8, 4), (3, 5), (6, 9)])
+@pytest.mark.parametrize("k,m", [(4, 2), (10, 4), (12, 2), (8, 4), (3, 5), (6, 9), (10, 5),
+                                 (12, 6), (8, 8)])
 def test_decode_reconstruct_random_erasures(amd, oracle, k, m):
     drv = amd(k=k, m=m, ec_type="liberasurecode_rs_vand")
     rng = random.Random(k * 31 + m)
@@ -99,7 +101,10 @@ def _batch_layout(k, m, n_obj, obj_len):
                                          (8, 3, 8 * 8192), (10, 4, 10 * 4096 + 2),
                                          # prime k: padded stream slots (NB = 4)
                                          (7, 3, 7 * 4096 * 5 + 13), (11, 4, 1 << 20),
-                                         (13, 3, (2 << 20) + 6)])
+                                         (13, 3, (2 << 20) + 6),
+                                         # one eight-row encode pass (m = 5..8)
+                                         (10, 5, 1 << 20), (12, 6, 999999), (8, 8, 8 * 4096 * 7 + 10),
+                                         (5, 7, 65536 + 6)])
 def test_batch_encode_decode_reconstruct(oracle, gpu, k, m, obj_len):
     import torch
     from pyeclib_amd import batch

@@ -2,14 +2,18 @@
 """A/B timing of the kernels' tuning switches, interleaved in one process.
 
 Each positional argument is one variant: "base" (no switches) or a
-comma-separated list of VAR=VAL environment settings, e.g.
-    python tools/ab_bench.py base ECAMD_DEC_OCC3=1 ECAMD_XCD=0
-The launcher reads the switches at every launch (ec_kernels_impl.hpp), so the
-variants run round-robin in one process on the same buffers (the workload of
-bench.py: k=10 m=4, 256 x 4 MiB, 4 erasures per object).  Every variant's
-decode output is checked against the objects and its parity against the
-first variant's.  Prints median / min microseconds per launch and GB/s of
-algorithmic bytes.
+comma-separated list of NAME=VAL switches, e.g.
+    python tools/ab_bench.py base ECAMD_ENC_R3=1,ECAMD_DEC_R3=1 ECAMD_XCD=0
+The switches exist only in the A/B build of the library (`make -C
+pyeclib_amd/csrc ab` -> tools/build/libpyeclib_amd_ab.so, which this tool
+loads): its launchers read them, by name, at every launch (ecamd_ab_set;
+ec_kernels_impl.hpp launch_*_ab), so the variants run round-robin in one
+process on the same buffers (the workload of bench.py: k=10 m=4, 256 x 4
+MiB, 4 erasures per object).  The product library has none of them.  Every
+variant's decode output is checked against the objects and its parity
+against the first variant's (except the memory-only NOCOMP probes, whose
+output is wrong by design).  Prints median / min microseconds per launch and
+GB/s of algorithmic bytes.
 """
 from __future__ import annotations
 
@@ -22,8 +26,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+AB_LIB = os.path.join(ROOT, "tools", "build", "libpyeclib_amd_ab.so")
 
-KEYS = ["ECAMD_XCD", "ECAMD_DEC_OCC3"]  # plus any other key a variant names
+KEYS = []  # every switch any variant names
 
 
 def parse_variant(text):
@@ -63,10 +68,19 @@ def main():
                          "each decode and the next encode, outside both kernels' events "
                          "(does the encode's alternation cost go away once the decode's "
                          "dirty Infinity-Cache lines are evicted by clean reads?)")
+    ap.add_argument("--lib", default=AB_LIB, help="A/B build of the library to load")
     args = ap.parse_args()
 
+    if not os.path.exists(args.lib):
+        sys.exit(f"{args.lib} missing: build it with `make -C pyeclib_amd/csrc ab`")
+    os.environ["PYECLIB_AMD_LIBRARY"] = args.lib
+    import ctypes
+
     import torch
-    from pyeclib_amd import batch
+    from pyeclib_amd import _native, batch
+    ab_set = _native.lib.ecamd_ab_set
+    ab_set.restype = ctypes.c_int
+    ab_set.argtypes = [ctypes.c_char_p, ctypes.c_int]
 
     k, m, n, B = args.k, args.m, args.obj_bytes, args.batch
     dev = torch.device("cuda:0")
@@ -102,15 +116,10 @@ def main():
     for _, env in variants:
         KEYS.extend(key for key in env if key not in KEYS)
     times = {v: {"enc": [], "dec": []} for v, _ in variants}
-    base_env = {key: os.environ.get(key) for key in KEYS}
 
     def apply(env):
         for key in KEYS:
-            if base_env[key] is None:
-                os.environ.pop(key, None)
-            else:
-                os.environ[key] = base_env[key]
-        os.environ.update(env)
+            ab_set(key.encode(), int(env[key]) if key in env else -1)
 
     for rnd in range(args.rounds):
         for name, env in variants:

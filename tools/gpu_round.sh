@@ -70,10 +70,6 @@ for s in $STEPS; do
     (cd $R && timeout -k 10 300 python3 bench.py --inline-crc32 --steps 20 --warmup 5 --no-host \
         --no-cpu-baseline > $O/bench_crc.json 2> $O/bench_crc.err)
     tail -c 400 $O/bench_crc.json ;;
-  crcntl)
-    (cd $R && ECAMD_CRC_NTL=1 timeout -k 10 300 python3 bench.py --inline-crc32 --steps 10 --no-host \
-        --no-cpu-baseline > $O/bench_crc_ntl.json 2> $O/bench_crc_ntl.err)
-    tail -c 400 $O/bench_crc_ntl.json ;;
   bench)
     (cd $R && timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err)
     cat $O/bench.json ;;

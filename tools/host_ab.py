@@ -90,6 +90,7 @@ def main():
         for key in KEYS:
             os.environ.pop(key, None)
         os.environ.update(env)
+        codec = batch.BatchCodec(k, m)  # the knobs are read when an instance is created
         te, td = [], []
         for r in range(args.reps + 1):
             hpar.zero_()

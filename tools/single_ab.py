@@ -30,9 +30,13 @@ def main():
     ap.add_argument("--sizes", default="65536,262144,1048576,4194304")
     a = ap.parse_args()
     from pyeclib_amd import ECDriver
-    drv = ECDriver(k=a.k, m=a.m, ec_type="liberasurecode_rs_vand")
     rng = np.random.default_rng(5)
     variants = {"dma": "0", "pinned": str(1 << 40)}
+    drivers = {}
+    for v, val in variants.items():  # the knob is read when an instance is created
+        os.environ["ECAMD_SINGLE_PINNED_MAX"] = val
+        drivers[v] = ECDriver(k=a.k, m=a.m, ec_type="liberasurecode_rs_vand")
+    os.environ.pop("ECAMD_SINGLE_PINNED_MAX", None)
     print(f"k={a.k} m={a.m}, median of {a.reps} calls, microseconds")
     print(f"{'size':>9} {'variant':>7} {'encode':>9} {'decode':>9} {'reconstruct':>12}")
     for n in [int(x) for x in a.sizes.split(",")]:
@@ -40,8 +44,8 @@ def main():
         t = {v: {"e": [], "d": [], "r": []} for v in variants}
         ref = None
         for _ in range(a.reps):
-            for v, val in variants.items():
-                os.environ["ECAMD_SINGLE_PINNED_MAX"] = val
+            for v in variants:
+                drv = drivers[v]
                 t0 = time.perf_counter()
                 frags = drv.encode(data)
                 t1 = time.perf_counter()
@@ -59,8 +63,8 @@ def main():
         for v in variants:
             med = {x: 1e6 * statistics.median(t[v][x]) for x in "edr"}
             print(f"{n:>9} {v:>7} {med['e']:9.1f} {med['d']:9.1f} {med['r']:12.1f}")
-    os.environ.pop("ECAMD_SINGLE_PINNED_MAX", None)
-    drv.close()
+    for drv in drivers.values():
+        drv.close()
 
 
 if __name__ == "__main__":
