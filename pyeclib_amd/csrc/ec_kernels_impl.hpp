@@ -793,10 +793,12 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
 // it, so every wave drained all NB of its in-flight loads at every item
 // boundary (round 4, found in the generated code).  With the entry path
 // shaped like the back edge the wait is vmcnt(NB - 1 + NR (+ data stores)),
-// and loads stay in flight across items.  HEAD = false keeps the old
-// prologue (A/B builds).
+// and loads stay in flight across items.  Measured (tools/ab_bench.py, same
+// process, profiles/r04e_ab.txt): encode 297.4 us with it against 285.7
+// without -- the deeper stream costs more at the HBM than the drain did --
+// so the encode keeps HEAD = false; decode (decode_interior) keeps its own.
 template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false, int CH = 1,
-          bool NTL = false, int NBX = 0, bool HEAD = true>
+          bool NTL = false, int NBX = 0, bool HEAD = false>
 __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
   constexpr int NB = NBX ? NBX : stream_bufs<K>();  // NBX: A/B (divides K)
   const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split, interior_block(p.edge_blocks));
@@ -907,7 +909,7 @@ __host__ __device__ constexpr int encode_occ() {
 }
 
 template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false, int CH = 1,
-          bool NTL = false, int NBX = 0, bool HEAD = true>
+          bool NTL = false, int NBX = 0, bool HEAD = false>
 __global__ void __launch_bounds__(kThreadsPerBlock)
     __attribute__((amdgpu_waves_per_eu(encode_occ<F, K, DATA, NBX>(), 8)))
     encode_kernel(EncodeParams p) {
@@ -931,6 +933,169 @@ __global__ void __launch_bounds__(kThreadsPerBlock) encode_edge_kernel(EncodePar
   load_tables(p.tables, K * F::kTableBytes, 0);
   __syncthreads();
   encode_edges<F, K, NR, false>(p, blockIdx.x, gridDim.x);
+}
+
+// ---------------- encode with a loader / consumer split (LDS-DMA ring) ----------------
+//
+// One 512-thread block (8 waves, two per SIMD) per CU.  An item is 8 KiB of
+// payload positions; a ring slot holds one input of one item (8 KiB).  Waves
+// 0-3 (one per SIMD) are the loaders: they move every input chunk from HBM
+// straight into the LDS ring with buffer_load_dwordx4 ... lds (1 KiB per
+// wave-instruction, no VGPRs held), R - 1 slots ahead.  All 8 waves consume:
+// each reads its 1 KiB of the slot from LDS (ds_read_b128), takes the nibble
+// lookups and, after the item's last input, stores its parity rows.  So HBM
+// sees 4 issuing waves per CU keeping (R - 1) x 8 KiB in flight, while the
+// lookups still have 2 waves per SIMD to hide behind.
+//
+// Ordering (MI355X_MICROARCH.md, LDS-DMA): slot t is read only after its
+// loaders' s_waitcnt vmcnt (their DMAs of slot t retired) and a barrier all
+// waves pass; the DMA of slot t + R - 1 overwrites ring[(t - 1) % R], issued
+// only after that same barrier, which every wave reaches after reading slot
+// t - 1.  The DMAs are inline asm (hipcc does not see them, so it neither
+// drains them before LDS reads nor counts them); the waits are explicit.
+// Edge items and headers run in blocks of their own, 256 threads of them.
+constexpr uint32_t kDmaSlot = 8192;  // bytes of a ring slot per KiB of SW (8 waves x 1 KiB)
+constexpr uint32_t kDmaThreads = 512;
+
+typedef unsigned int v4u_s __attribute__((ext_vector_type(4)));
+// Buffer descriptor in SGPRs as the 4 dwords of the V# (gfx9: base, stride 0,
+// num_records, dword3 as __builtin_amdgcn_make_buffer_rsrc builds it).
+__device__ __forceinline__ v4u_s rsrc4(const void* base, uint32_t records) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  v4u_s r;
+  r.x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  r.y = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32)) & 0xFFFFu;
+  r.z = to_sgpr(records);
+  r.w = 0x00020000u;
+  return r;
+}
+// 16 B per lane from buffer r at voff + soff into LDS at lds + 16 * lane.
+template <bool NT>
+__device__ __forceinline__ void dma16(v4u_s r, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  if constexpr (NT)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ void ring_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");  // no LDS read of the slot moves above the barrier
+}
+
+template <class F, int K>
+__host__ __device__ constexpr uint32_t dma_ring_base() {
+  return (K * F::kTableBytes + 255u) & ~255u;
+}
+// SW: KiB of each slot a consumer wave takes (slot = 8 * SW KiB, item = one
+// slot's positions across the k inputs); L: loader waves.
+template <class F, int K, int R, int SW, int W = 8>
+__host__ __device__ constexpr uint32_t dma_lds_bytes() {
+  return dma_ring_base<F, K>() + R * 1024 * W * SW;
+}
+
+// W: waves per block (8 = 2 per SIMD, 16 = 4 per SIMD).  DATA: the consumers
+// also store each slot they read from LDS into its data fragment.
+template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
+          bool DATA = false>
+__global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
+  static_assert(R >= 2 && R <= K + 1, "ring of 2 .. K + 1 slots");
+  static_assert(L == 2 || L == 4 || L == 8 || L == 16, "loader waves");
+  constexpr uint32_t kSlot = 1024u * W * SW;       // bytes of one ring slot
+  constexpr int kPerLoader = kSlot / 1024 / L;    // DMA wave-instructions per loader and slot
+  const uint32_t wave = wave_in_block();
+  if (blockIdx.x < p.edge_blocks) {  // edge items and headers: 256 threads
+    if (threadIdx.x >= kThreadsPerBlock) return;
+    for (uint32_t i = threadIdx.x; i < K * F::kTableBytes / 16; i += kThreadsPerBlock)
+      lds_v4(0)[i] = reinterpret_cast<const v4u*>(p.tables)[i];
+    __syncthreads();
+    encode_edges<F, K, NR, DATA>(p, blockIdx.x, p.edge_blocks);
+    return;
+  }
+  for (uint32_t i = threadIdx.x; i < K * F::kTableBytes / 16; i += W * 64)
+    lds_v4(0)[i] = reinterpret_cast<const v4u*>(p.tables)[i];
+  __syncthreads();
+  const ItemRange rg = item_range(p.n_obj * p.tiles, p.xcd_split, interior_block(p.edge_blocks));
+  if (rg.begin >= rg.end) return;  // block-uniform
+  const uint32_t n_items = to_sgpr((rg.end - rg.begin + rg.step - 1) / rg.step);
+  const bool loader = wave < static_cast<uint32_t>(L);
+  const uint32_t lane16 = lane_id() * 16;
+  constexpr uint32_t kRing = dma_ring_base<F, K>();
+  // item i of this block: object and first payload position
+  auto item_at = [&](uint32_t i, uint32_t& o, uint32_t& x0) {
+    const uint32_t w = rg.begin + i * rg.step;
+    o = to_sgpr(w / p.tiles);
+    x0 = (w - o * p.tiles) * kSlot;
+  };
+  // loaders: the DMAs of slot (item i, input j) into ring slot `ri`
+  auto issue = [&](uint32_t i, int j, uint32_t ri) {
+    if (!loader) return;
+    uint32_t o, x0;
+    const bool valid = i < n_items;
+    item_at(valid ? i : 0, o, x0);
+    const v4u_s src = rsrc4(p.objs + static_cast<uint64_t>(o) * p.obj_stride, valid ? ~0u : 0u);
+    const uint32_t part = wave * (kSlot / L);
+    const uint32_t lds = kRing + ri * kSlot + part;
+    const uint32_t soff = to_sgpr(j * p.bs + x0 + part);
+#pragma unroll
+    for (int c = 0; c < kPerLoader; ++c) dma16<NT>(src, lane16, soff + 1024 * c, lds + 1024 * c);
+  };
+  // prologue: slots 0 .. R-2
+#pragma unroll
+  for (int t = 0; t < R - 1; ++t) issue(t / K, t % K, t);
+  uint32_t ring = 0;  // ring slot of the current slot t
+  typename F::Acc s[SW];
+#pragma unroll
+  for (int c = 0; c < SW; ++c) F::zero(s[c]);
+#pragma clang loop unroll(disable)
+  for (uint32_t i = 0; i < n_items; ++i) {
+    uint32_t o, x0;
+    item_at(i, o, x0);
+    const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
+    Rsrc dat;
+    if constexpr (DATA) dat = rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      // (vmcnt counts the data-fragment stores too: the wait is then
+      // conservative, never short -- loads retire in order)
+      if (loader) wait_vm<kPerLoader * (R - 2)>();  // this wave's DMAs of slot t retired
+      ring_barrier();                                // ... everyone's; ring[t-1] read by all
+      // slot t + R - 1 = (item i + (j + R - 1) / K, input (j + R - 1) % K)
+      const uint32_t rn = ring == 0 ? R - 1 : ring - 1;
+      issue(i + (j + R - 1) / K, (j + R - 1) % K, rn);
+#pragma unroll
+      for (int c = 0; c < SW; ++c) {
+        const v4u xin = *lds_v4(kRing + ring * kSlot + (wave * SW + c) * 1024 + lane16);
+        const uint4 x = make_uint4(xin.x, xin.y, xin.z, xin.w);
+        F::template mac<true>(F::kb(0), j * F::kTableBytes, x, s[c]);
+        if constexpr (DATA)
+          buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x0 + (wave * SW + c) * 1024, x);
+      }
+      ring = ring + 1 == R ? 0 : ring + 1;
+    }
+#pragma unroll
+    for (int c = 0; c < SW; ++c) {
+      F::pin(s[c]);
+      const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x0 + (wave * SW + c) * 1024;
+#pragma unroll
+      for (int q = 0; q < NR; ++q)
+        buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, F::row(s[c], q));
+      F::zero(s[c]);
+    }
+  }
+  if (loader) wait_vm<0>();  // no DMA may land in LDS after the block ends
 }
 
 // ---------------- encode with the parity CRC fused (inline_crc32) ----------------
@@ -1717,12 +1882,41 @@ hipError_t launch_encode_crc(EncodeParams p, Kern kern, int per_cu, uint32_t edg
   return launch_crc_finish(fp, stream);
 }
 
+// The loader / consumer encode (encode_dma_kernel): one W * 64-thread block
+// per CU (a multiple of 8, so blocks keep their XCD) after E edge blocks.
+// Measured round 4 (tools/ab_bench.py, same process, k = 10, m = 4,
+// 256 x 4 MiB, profiles/r04e_ab.txt): R = 3, W = 16 (four consumer waves per
+// SIMD, 16 KiB slots), L = 4 loaders 271.5 us against 285.7 for the stream
+// kernel; R = 3 SW = 2 276.4, R = 5 280.6, R = 4 W = 16 274.6, L = 8 273.4.
+// The default path takes it for k >= kDmaMinK when the batch has an item of
+// 16 KiB for every CU (smaller batches keep the stream kernel's 4 KiB items).
+constexpr int kDmaMinK = 4;
+constexpr uint32_t kDmaItem = 16 * 1024;
+template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
+          bool DATA = false>
+hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream) {
+  set_tiles(p, last_room(p.bs, p.obj_len, K), 1024u * W * SW / kTile);
+  const auto kern = encode_dma_kernel<F, K, NR, R, NT, L, SW, W, DATA>;
+  constexpr size_t lds = dma_lds_bytes<F, K, R, SW, W>();
+  if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
+  const int cus = device_cus();
+  const uint32_t items = p.n_obj * p.tiles;
+  const uint32_t edge_items = std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u);
+  const uint32_t e = (std::min<uint32_t>(edge_items, static_cast<uint32_t>(cus)) + 7u) & ~7u;
+  uint32_t g = std::min<uint32_t>(static_cast<uint32_t>(cus) & ~7u, std::max(items, 1u));
+  if (g >= 8) g &= ~7u;
+  p.edge_blocks = edge_items ? e : 0;
+  p.fused_edges = 1;
+  p.xcd_split = xcd_split_for(static_cast<int>(g), true);
+  hipLaunchKernelGGL(kern, dim3(g + p.edge_blocks), dim3(W * 64), lds, stream, p);
+  return hipGetLastError();
+}
+
 // A/B builds: the alternative encode launches of past measurements (the
 // switches are documented where each one was measured: DESIGN.md §4).
 // Returns hipErrorNotSupported when no switch applies to this launch.
 template <class F, int K, int NR>
 hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint32_t edge_items) {
-  const int64_t room = last_room(p.bs, p.obj_len, K);
   constexpr size_t lds = K * F::kTableBytes;
   const int per_cu = ab_knob("ECAMD_ENC_PER_CU", kEncodePerCu);
   if (p.crc_tables != nullptr) {
@@ -1760,31 +1954,29 @@ hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint3
   }
   if constexpr (K == 10 && NR == 4) {
     const bool ntl = ab_knob("ECAMD_ENC_NTL", 0);
+    if (!data) {
+      // loader / consumer split: ring slots R, loader waves L, KiB per consumer wave SW
+      const int ring = ab_knob("ECAMD_ENC_DMA", 0);
+      const int lw = ab_knob("ECAMD_ENC_DMA_L", 4), sw = ab_knob("ECAMD_ENC_DMA_SW", 1);
+      const int nw = ab_knob("ECAMD_ENC_DMA_W", 8);
+      if (ring == 5 && lw == 4 && sw == 1 && nw == 8) return launch_encode_dma<F, K, NR, 5, true>(p, stream);
+      if (ring == 3 && lw == 4 && sw == 2 && nw == 8) return launch_encode_dma<F, K, NR, 3, true, 4, 2>(p, stream);
+      if (ring == 3 && lw == 8 && sw == 2 && nw == 8) return launch_encode_dma<F, K, NR, 3, true, 8, 2>(p, stream);
+      if (ring == 2 && lw == 4 && sw == 4 && nw == 8) return launch_encode_dma<F, K, NR, 2, true, 4, 4>(p, stream);
+      if (ring == 3 && lw == 4 && sw == 4 && nw == 8) return launch_encode_dma<F, K, NR, 3, true, 4, 4>(p, stream);
+      if (ring == 3 && lw == 4 && sw == 1 && nw == 16) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16>(p, stream);
+      if (ring == 3 && lw == 8 && sw == 1 && nw == 16) return launch_encode_dma<F, K, NR, 3, true, 8, 1, 16>(p, stream);
+      if (ring == 4 && lw == 4 && sw == 1 && nw == 16) return launch_encode_dma<F, K, NR, 4, true, 4, 1, 16>(p, stream);
+      if (ring == 3 && lw == 4 && sw == 2 && nw == 16) return launch_encode_dma<F, K, NR, 3, true, 4, 2, 16>(p, stream);
+    }
     if (ab_knob("ECAMD_ENC_NOCOMP", 0))  // memory-only probe: WRONG parity
       return ntl ? launch_edges_apart(encode_kernel<F, K, NR, true, false, 1, true>, p, lds, items,
                                       edge_items, stream, per_cu, true)
                  : launch_edges_apart(encode_kernel<F, K, NR, true>, p, lds, items, edge_items,
                                       stream, per_cu, true);
-    if (!data) {
-      if (ab_knob("ECAMD_ENC_R3", 0))  // the round-3 prologue (item-boundary drain)
-        return launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, false, 0, false>, p, lds,
-                                  items, edge_items, stream, per_cu, true);
-      const int ch = ab_knob("ECAMD_ENC_CH", 1);
-      const int nb = ab_knob("ECAMD_ENC_NB", 0);  // 10: every input of an item in flight
-      if (nb == 10)
-        return ntl ? launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, true, 10>, p, lds, items, edge_items, stream, per_cu, true)
-                   : launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, false, 10>, p, lds, items, edge_items, stream, per_cu, true);
-      if (ch == 2) {
-        set_tiles(p, room, 2);
-        const uint32_t items2 = p.n_obj * p.tiles;
-        const uint32_t edges2 = std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u);
-        return ntl ? launch_edges_apart(encode_kernel<F, K, NR, false, false, 2, true>, p, lds, items2, edges2, stream, per_cu, true)
-                   : launch_edges_apart(encode_kernel<F, K, NR, false, false, 2, false>, p, lds, items2, edges2, stream, per_cu, true);
-      }
-      if (ntl)
-        return launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, true>, p, lds, items,
-                                  edge_items, stream, per_cu, true);
-    }
+    if (!data && ab_knob("ECAMD_ENC_R3", 0))  // the round-3 prologue (item-boundary drain)
+      return launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, false, 0, false>, p, lds,
+                                items, edge_items, stream, per_cu, true);
   }
   if (per_cu != kEncodePerCu)
     return data ? launch_edges_apart(encode_kernel<F, K, NR, false, true>, p, lds, items,
@@ -1810,6 +2002,14 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     const hipError_t e = launch_encode_ab<F, K, NR>(p, stream, data, edge_items);
     if (e != hipErrorNotSupported) return e;
   }
+  if constexpr (kAB && F::kRows > kRowsPerPass) {  // eight-row encode: blocks per CU
+    const int per_cu = ab_knob("ECAMD_ENC_PER_CU", kEncodePerCu);
+    if (per_cu != kEncodePerCu && !data && p.crc_tables == nullptr) {
+      p.fused_edges = 1;
+      return launch_edges_apart(encode_kernel<F, K, NR>, p, lds, p.n_obj * p.tiles, edge_items,
+                                stream, per_cu, true);
+    }
+  }
   if (p.crc_tables != nullptr) {
     if constexpr (F::kRows > kRowsPerPass) {
       return hipErrorInvalidValue;  // the fused CRC runs in four-row passes
@@ -1819,6 +2019,15 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
                   : launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR>, kEncodePerCu,
                                                 edge_items, stream);
     }
+  }
+  // the loader / consumer encode (encode_dma_kernel) for k >= kDmaMinK; its
+  // input offsets j * bs + x are 32-bit
+  if constexpr (F::kRows <= kRowsPerPass && K >= kDmaMinK) {
+    const uint64_t dma_items = static_cast<uint64_t>(std::max<int64_t>(room, 0)) / kDmaItem * p.n_obj;
+    if (dma_items >= static_cast<uint64_t>(device_cus()) &&
+        static_cast<uint64_t>(K) * p.bs + 65536u <= 0xFFFFFFFFull && !ab_knob("ECAMD_ENC_STREAM", 0))
+      return data ? launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, true>(p, stream)
+                  : launch_encode_dma<F, K, NR, 3, true, 4, 1, 16>(p, stream);
   }
   p.fused_edges = 1;
   const uint32_t items = p.n_obj * p.tiles;

@@ -106,7 +106,13 @@ struct Knobs {
   // and r02n, k=10 m=4): faster than the DMA path up to 1 MiB on both boxes
   // -- 64 KiB encode 51-54 vs 97-105 us, decode 57-59 vs 91-93; 1 MiB 148 vs
   // 181-187, 163-167 vs 264-268.
-  size_t single_pinned_max = size_t(1) << 20;  // ECAMD_SINGLE_PINNED_MAX
+  // Round 4 (tools/single_probe.py, profiles/r04e_single_probe.txt): with the
+  // parallel host copies, 4 MiB encode 279 -> 215 us through pinned staging.
+  size_t single_pinned_max = size_t(64) << 20;  // ECAMD_SINGLE_PINNED_MAX
+  // the kernels read the caller's object (encode) and write the caller's
+  // output (decode) in place, registered with hipHostRegister for the call
+  // (about 3 us for 4 MiB) instead of copying through the staging buffer
+  bool register_caller = true;  // ECAMD_REGISTER_CALLER=0: always copy
   long pool_slots = 0;          // ECAMD_POOL_SLOTS: decode table-set slots (0 = from 32 MiB)
   bool host_staged = false;     // ECAMD_HOST_STAGED: copy-engine host pipeline
   bool host_staged_out = false; // ECAMD_HOST_STAGED_OUT: ... with outputs staged through HBM
@@ -125,6 +131,7 @@ struct Knobs {
     k.host_chunk_mb = static_cast<int>(std::max<long>(1, env_long("ECAMD_HOST_CHUNK_MB", k.host_chunk_mb)));
     k.edge_blocks = env_on("ECAMD_EDGE_BLOCKS", true);
     k.crc_fused = env_on("ECAMD_CRC_FUSED", true);
+    k.register_caller = env_on("ECAMD_REGISTER_CALLER", true);
     return k;
   }
 };
@@ -1436,13 +1443,6 @@ int liberasurecode_instance_destroy(int desc) {
 
 namespace {
 
-// liberasurecode_encode's work for one object, into k + m caller-provided
-// fragments of bs + 80 bytes (caller holds I.mu, device set).  The object is
-// copied into pinned, device-mapped staging (host_copy: parallel for large
-// objects) and the kernel reads it there over PCIe; while it runs, the host
-// fills the data fragments from the caller's object (prepare_fragments_for_
-// encode's copy), then copies the parity out.  Objects past the
-// single_pinned_max knob take DMA copies through HBM instead.
 // Phase clock of the single-object calls (Instance::phase_us).
 struct PhaseClock {
   double* out;
@@ -1457,6 +1457,47 @@ struct PhaseClock {
   }
 };
 
+// A caller's host buffer the kernels use in place for one call: registered
+// (mapped) with hipHostRegister, unregistered when the guard ends -- after
+// the call's stream synchronize.  pin() fails, and the caller copies through
+// the staging buffer instead, when the range cannot be registered (its pages
+// already are, or the range runs into unmapped memory).
+struct CallerPin {
+  void* host = nullptr;
+  uint8_t* dev = nullptr;
+  bool pin(const void* p, size_t n) {
+    if (n == 0) return false;
+    void* h = const_cast<void*>(p);
+    if (hipHostRegister(h, n, hipHostRegisterMapped) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || d == nullptr) {
+      (void)hipGetLastError();
+      (void)hipHostUnregister(h);
+      return false;
+    }
+    host = h;
+    dev = static_cast<uint8_t*>(d);
+    return true;
+  }
+  CallerPin() = default;
+  CallerPin(const CallerPin&) = delete;
+  CallerPin& operator=(const CallerPin&) = delete;
+  ~CallerPin() {
+    if (host) (void)hipHostUnregister(host);
+  }
+};
+
+// liberasurecode_encode's work for one object, into k + m caller-provided
+// fragments of bs + 80 bytes (caller holds I.mu, device set).  The kernel
+// reads the caller's object in place over PCIe (CallerPin) -- or, when it
+// does not register, a copy in pinned, device-mapped staging (host_copy:
+// parallel for large objects); while it runs, the host fills the data
+// fragments from the object (prepare_fragments_for_encode's copy), then
+// copies the parity out.  Objects past the single_pinned_max knob that do not
+// register take DMA copies through HBM instead.
 int encode_into(Instance& I, const char* data, uint64_t len, uint8_t* const* frags) {
   const int k = I.k, m = I.m;
   PhaseClock clk(I.phase_us);
@@ -1478,16 +1519,23 @@ int encode_into(Instance& I, const char* data, uint64_t len, uint8_t* const* fra
   if (bs > 0) {
     const uint64_t fs = round16(kHeaderBytes + round16(bs));
     const uint64_t obj_bytes = round16(len);
-    uint8_t* pin = len <= I.knobs.single_pinned_max ? I.pin.ensure(obj_bytes + fs * m) : nullptr;
+    // the object in place when it registers (through round16(len): the edge
+    // items read whole 16-B units), the parity through the staging buffer
+    // (its stores fill whole 16-B units past bs)
+    CallerPin src;
+    const bool direct = I.knobs.register_caller && src.pin(data, obj_bytes);
+    const uint64_t staged = direct ? 0 : obj_bytes;
+    uint8_t* pin = len <= I.knobs.single_pinned_max ? I.pin.ensure(staged + fs * m) : nullptr;
     hipError_t e = hipSuccess;
-    if (!pin && (e = I.scratch.ensure(obj_bytes + fs * m)) != hipSuccess) return hip_errno(e);
-    uint8_t* d_obj = pin ? pin : I.scratch.b();
-    uint8_t* d_par = d_obj + obj_bytes;
-    if (pin) {
+    if (!pin && (e = I.scratch.ensure(staged + fs * m)) != hipSuccess) return hip_errno(e);
+    uint8_t* base = pin ? pin : I.scratch.b();
+    uint8_t* d_obj = direct ? src.dev : base;
+    uint8_t* d_par = base + staged;
+    if (!direct && pin) {
       const CopyJob in[2] = {{d_obj, data, len}, {d_obj + len, nullptr, obj_bytes - len}};
       host_copy(in, 2);
-    } else if ((e = hipMemcpyAsync(d_obj, data, len, hipMemcpyHostToDevice, I.stream)) !=
-               hipSuccess) {
+    } else if (!direct && (e = hipMemcpyAsync(d_obj, data, len, hipMemcpyHostToDevice,
+                                              I.stream)) != hipSuccess) {
       return hip_errno(e);
     }
     clk.mark(0);
@@ -1712,12 +1760,16 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
   }
   const uint64_t fs = round16(kHeaderBytes + round16(bs));
   const uint64_t obj_bytes = round16(orig);
-  const size_t need = fs * (k + I.m) + obj_bytes;
+  // the decoded object straight into the caller's buffer when it registers
+  // (the kernels' object stores are byte-exact at its end)
+  CallerPin dst;
+  const bool direct = I.knobs.register_caller && dst.pin(out, orig);
+  const size_t need = fs * (k + I.m) + (direct ? 0 : obj_bytes);
   uint8_t* pin = orig <= I.knobs.single_pinned_max ? I.pin.ensure(need) : nullptr;
   hipError_t e = hipSuccess;
   if (!pin && (e = I.scratch.ensure(need)) != hipSuccess) return hip_errno(e);
   uint8_t* d_frags = pin ? pin : I.scratch.b();
-  uint8_t* d_obj = d_frags + fs * (k + I.m);
+  uint8_t* d_obj = direct ? dst.dev : d_frags + fs * (k + I.m);
   uint32_t mask = 0;
   int rc = stage_fragments(I, D.P, bs, fs, d_frags, &mask, pin != nullptr);
   clk.mark(0);
@@ -1725,13 +1777,13 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
     DecodeJob J{d_frags, fs, fs * (k + I.m), orig, d_obj, obj_bytes, 1, &mask, nullptr, nullptr};
     rc = run_decode(I, J, I.stream);
   }
-  if (rc == 0 && orig && !pin)
+  if (rc == 0 && orig && !pin && !direct)
     if ((e = hipMemcpyAsync(out, d_obj, orig, hipMemcpyDeviceToHost, I.stream)) != hipSuccess)
       rc = hip_errno(e);
   clk.mark(1);
   if ((e = hipStreamSynchronize(I.stream)) != hipSuccess && rc == 0) rc = hip_errno(e);
   clk.mark(3);
-  if (rc == 0 && orig && pin) host_copy(out, d_obj, orig);
+  if (rc == 0 && orig && pin && !direct) host_copy(out, d_obj, orig);
   clk.mark(4);
   return rc;
 }

@@ -14,7 +14,8 @@
 namespace ecamd {
 namespace {
 
-constexpr size_t kParallelMin = 256 << 10;  // smaller copies stay on the caller
+constexpr size_t kParallelMin = 2 << 20;  // smaller copies stay on the caller (r04e: the
+                                          // pool's wake-up costs more at 1 MiB)
 constexpr size_t kPiece = 64 << 10;
 
 struct Piece {

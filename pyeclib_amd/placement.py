@@ -76,8 +76,13 @@ def kfd_gpus(sysfs: str = "/sys") -> list[str]:
 def _visible(order: list, env: dict) -> list:
     """Narrow a device list by the runtime's visibility variables (index
     lists only; a UUID list -- or an index out of range -- gives [] and the
-    caller does not bind)."""
-    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+    caller does not bind).  ROCR_VISIBLE_DEVICES applies first (the ROCr
+    runtime's filter), then HIP_VISIBLE_DEVICES; HIP honours
+    CUDA_VISIBLE_DEVICES only when HIP_VISIBLE_DEVICES is unset, so the two
+    never narrow the list twice."""
+    hip = env.get("HIP_VISIBLE_DEVICES")
+    hip_set = hip is not None and hip.strip() != ""
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES" if hip_set else "CUDA_VISIBLE_DEVICES"):
         v = env.get(var)
         if v is None or v.strip() == "":
             continue

@@ -65,6 +65,18 @@ def test_visible_devices_remap(tmp_path):
     assert "reason" in placement.gpu_numa(0, sysfs, env={"HIP_VISIBLE_DEVICES": "GPU-abcd"})
 
 
+def test_hip_and_cuda_visible_both_set(tmp_path):
+    """A launcher that sets HIP_VISIBLE_DEVICES and CUDA_VISIBLE_DEVICES to the
+    same list: HIP applies only the former (CUDA_VISIBLE_DEVICES is read only
+    when HIP_VISIBLE_DEVICES is unset), so the list is narrowed once."""
+    sysfs = fake_sysfs(tmp_path)
+    env = {"HIP_VISIBLE_DEVICES": "1,2", "CUDA_VISIBLE_DEVICES": "1,2"}
+    assert placement.gpu_numa(0, sysfs, env=env)["pci"] == "0000:85:00.0"
+    assert placement.gpu_numa(1, sysfs, env=env)["pci"] == "0001:0c:00.0"
+    # CUDA_VISIBLE_DEVICES alone still narrows
+    assert placement.gpu_numa(0, sysfs, env={"CUDA_VISIBLE_DEVICES": "2"})["pci"] == "0001:0c:00.0"
+
+
 def test_bind_intersects_affinity(tmp_path):
     sysfs = fake_sysfs(tmp_path)
     allowed = set(os.sched_getaffinity(0))

@@ -7,9 +7,12 @@ times of that call (ecamd_call_phases: staging copy in, launch, host work
 beside the kernel, wait for the kernel, copy out, headers), and the Python
 part (allocating the output bytes objects).  With --threads the probe
 re-runs itself in a child process per ECAMD_COPY_THREADS value (the copy
-pool is sized once per process).
+pool is sized once per process); --pinned does the same for
+ECAMD_SINGLE_PINNED_MAX (objects up to it stage through pinned memory, larger
+ones through DMA copies), both read when the process / instance starts.
 
-    python tools/single_probe.py [--sizes 1048576,4194304] [--threads 0,4,8] [--reps 30]
+    python tools/single_probe.py [--sizes 1048576,4194304] [--threads 0,4,8]
+                                 [--pinned 1048576,1073741824] [--reps 30]
 """
 from __future__ import annotations
 
@@ -65,25 +68,63 @@ def probe(sizes, reps, k=10, m=4):
                          "phases_us": {p: round(statistics.median(v), 1) for p, v in phases.items()},
                          "alloc_outputs_us": round(statistics.median(alloc), 1)})
     drv.close()
+    try:
+        rows.append(register_cost(sizes, reps))
+    except Exception as exc:  # noqa: BLE001 -- a probe, not a check
+        rows.append({"op": "host_register", "error": repr(exc)})
     return rows
+
+
+def register_cost(sizes, reps):
+    """What pinning the caller's own buffer would cost instead of copying it:
+    hipHostRegister (mapped) + hipHostGetDevicePointer + hipHostUnregister on
+    a fresh bytes object of each size (median of `reps`)."""
+    import numpy as np
+    hip = ctypes.CDLL(None)  # the HIP runtime the library was loaded against (RTLD_GLOBAL)
+    out = {"op": "host_register"}
+    for n in sizes:
+        ts = []
+        for i in range(reps):
+            b = np.random.default_rng(i).integers(0, 256, n, dtype=np.uint8).tobytes()
+            ptr = ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p)
+            dptr = ctypes.c_void_p()
+            t0 = time.perf_counter()
+            rc1 = hip.hipHostRegister(ptr, ctypes.c_size_t(n), ctypes.c_uint(2))  # mapped
+            rc2 = hip.hipHostGetDevicePointer(ctypes.byref(dptr), ptr, ctypes.c_uint(0))
+            t1 = time.perf_counter()
+            rc3 = hip.hipHostUnregister(ptr)
+            t2 = time.perf_counter()
+            if rc1 or rc2 or rc3:
+                out[f"{n}_error"] = [rc1, rc2, rc3]
+                break
+            ts.append((1e6 * (t1 - t0), 1e6 * (t2 - t1)))
+        if ts:
+            out[f"{n}_register_us"] = round(statistics.median(t[0] for t in ts), 1)
+            out[f"{n}_unregister_us"] = round(statistics.median(t[1] for t in ts), 1)
+    return out
 
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--sizes", default=f"{1 << 20},{4 << 20}")
     ap.add_argument("--threads", default="")
+    ap.add_argument("--pinned", default="")
     ap.add_argument("--reps", type=int, default=30)
     a = ap.parse_args()
     sizes = [int(x) for x in a.sizes.split(",")]
-    if not a.threads:
+    if not a.threads and not a.pinned:
         for r in probe(sizes, a.reps):
             r["copy_threads"] = os.environ.get("ECAMD_COPY_THREADS", "default")
+            r["pinned_max"] = os.environ.get("ECAMD_SINGLE_PINNED_MAX", "default")
             print(json.dumps(r), flush=True)
         return
-    for t in a.threads.split(","):
-        env = dict(os.environ, ECAMD_COPY_THREADS=t)
-        subprocess.run([sys.executable, __file__, "--sizes", a.sizes, "--reps", str(a.reps)],
-                       env=env, check=True)
+    for t in (a.threads or "4").split(","):
+        for pm in (a.pinned or "default").split(","):
+            env = dict(os.environ, ECAMD_COPY_THREADS=t)
+            if pm != "default":
+                env["ECAMD_SINGLE_PINNED_MAX"] = pm
+            subprocess.run([sys.executable, __file__, "--sizes", a.sizes, "--reps", str(a.reps)],
+                           env=env, check=True)
 
 
 if __name__ == "__main__":
