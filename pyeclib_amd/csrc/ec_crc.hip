@@ -178,16 +178,18 @@ __global__ void __launch_bounds__(256) crc_finish_kernel(CrcFinishParams p) {
       const uint32_t* part = p.part + static_cast<uint64_t>(o) * total * p.m + row;
       uint32_t acc = edge;
       if (p.tiles != 0) {
-        // the runs of object o's interior tiles: cut at the launch's block ranges
-        const uint64_t n = static_cast<uint64_t>(p.n_obj) * p.tiles;
-        const uint64_t lo = static_cast<uint64_t>(o) * p.tiles, hi = lo + p.tiles;
+        // the runs of object o's interior items (tile_ch tiles each): cut at
+        // the launch's block ranges
+        const uint32_t ch = p.tile_ch, items = p.tiles / ch;
+        const uint64_t n = static_cast<uint64_t>(p.n_obj) * items;
+        const uint64_t lo = static_cast<uint64_t>(o) * items, hi = lo + items;
         uint32_t b = static_cast<uint32_t>(lo * p.grid / n);
         while (b > 0 && run_begin(n, b, p.grid) > lo) --b;
         while (b + 1 < p.grid && run_begin(n, b + 1, p.grid) <= lo) ++b;
         for (uint64_t s = lo; s < hi; ++b) {
           const uint64_t e = std::min<uint64_t>(b + 1 < p.grid ? run_begin(n, b + 1, p.grid) : n, hi);
           if (e <= s) continue;  // empty block range
-          const uint32_t t0 = static_cast<uint32_t>(s - lo), t1 = static_cast<uint32_t>(e - lo);
+          const uint32_t t0 = static_cast<uint32_t>(s - lo) * ch, t1 = static_cast<uint32_t>(e - lo) * ch;
           acc ^= shift_tiles(part[static_cast<uint64_t>(t0) * p.m], total - t1);
           s = e;
         }

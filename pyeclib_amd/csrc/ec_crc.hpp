@@ -39,6 +39,8 @@ struct CrcFinishParams {
   const void* tables;       // CrcFinishTables for (bs, tiles + edge_tiles), device memory
   uint32_t n_obj, m, row0, nrows;
   uint32_t bs, tiles, edge_tiles, grid;
+  uint32_t tile_ch;         // 4 KiB tiles per interior item of the encode launch (runs
+                            // are cut at item boundaries; `tiles` counts 4 KiB tiles)
 };
 hipError_t launch_crc_finish(const CrcFinishParams& p, hipStream_t stream);
 

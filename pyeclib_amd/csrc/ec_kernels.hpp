@@ -124,6 +124,7 @@ struct DecodeParams {
   uint32_t fused_edges;        // set by the launcher: edge items run in the interior launch
   uint32_t edge_blocks;        // set by the launcher (see EncodeParams)
   uint32_t no_edge_blocks;     // caller (see EncodeParams)
+  uint32_t tile_ch;            // set by the launcher: 4 KiB tiles per interior item
 };
 
 // Dispatch on (p.w, p.k) to the per-k instantiations (ec_dispatch.cpp).

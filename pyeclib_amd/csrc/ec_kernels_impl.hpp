@@ -1163,7 +1163,8 @@ __device__ __forceinline__ void crc_block_flush(uint32_t (&acc)[NR], uint32_t ba
 
 // Run partials of object o from tile `tile` on, rows row0.. (ec_crc.hpp layout).
 __device__ __forceinline__ uint32_t* crc_part_at(const EncodeParams& p, uint32_t o, uint32_t tile) {
-  return p.crc_part + (static_cast<uint64_t>(o) * (p.tiles + p.edge_tiles) + tile) * p.m + p.row0;
+  const uint64_t total = p.tiles * p.tile_ch + p.edge_tiles;
+  return p.crc_part + (static_cast<uint64_t>(o) * total + tile) * p.m + p.row0;
 }
 
 // Interior with the parity CRC: block b streams the contiguous items
@@ -1268,6 +1269,142 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
     return;
   }
   encode_crc_interior<F, K, NR, DATA, NTL>(p);
+}
+
+// The parity CRC fused into the loader / consumer encode (encode_dma_kernel's
+// shape, W = 16 waves, 16 KiB items).  Block b streams the contiguous items
+// [N b / G, N (b + 1) / G) (crc_finish_kernel cuts the runs there), so a
+// thread's consecutive pieces of a parity payload are 16 KiB apart: acc =
+// Z_16384(acc) ^ raw16(piece).  A run's flush joins each wave's 64 lanes with
+// the lane tree (Z_16 .. Z_512) and the 16 waves with Z_1024 .. Z_8192, and
+// stores one raw CRC per row at the run's first 4 KiB tile.  The CRC lookups
+// run in the consumer waves while the loaders keep the ring full.
+constexpr uint32_t kCrcZ8192 = offsetof(CrcTables, z8192);
+constexpr uint32_t kCrcZ16384 = offsetof(CrcTables, z16384);
+template <class F, int K, int R>
+__host__ __device__ constexpr uint32_t crc_dma_lds_bytes() {
+  // GF tables, CRC maps, 16 waves x 4 rows of partials, the ring
+  return crc_lds_base<F, K>() + ((kCrcLdsBytes + 16 * 4 * 4 + 255u) & ~255u) + R * 16384u;
+}
+template <class F, int K, int NR, int R, bool NT, bool DATA = false>
+__global__ void __launch_bounds__(1024) encode_crc_dma_kernel(EncodeParams p) {
+  constexpr int W = 16, L = 4;
+  constexpr uint32_t kSlot = 1024u * W;
+  constexpr int kPerLoader = W / L;
+  constexpr uint32_t base = crc_lds_base<F, K>();
+  constexpr uint32_t red = base + kCrcLdsBytes;
+  constexpr uint32_t kRing = crc_dma_lds_bytes<F, K, R>() - R * kSlot;
+  load_tables(p.tables, K * F::kTableBytes, 0);
+  load_tables(static_cast<const uint32_t*>(p.crc_tables), kCrcLdsBytes, base);
+  __syncthreads();
+  if (blockIdx.x < p.edge_blocks) {  // edge items and headers: 256 threads
+    if (threadIdx.x >= kThreadsPerBlock) return;
+    encode_edges<F, K, NR, DATA>(p, blockIdx.x, p.edge_blocks);
+    return;
+  }
+  const uint32_t wave = wave_in_block(), lane = lane_id();
+  const uint64_t nall = static_cast<uint64_t>(p.n_obj) * p.tiles;
+  const IBlock ib = interior_block(p.edge_blocks);
+  const uint32_t begin = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nall * ib.b / ib.g));
+  const uint32_t end = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nall * (ib.b + 1) / ib.g));
+  if (begin >= end) return;  // block-uniform
+  const uint32_t n_items = end - begin;
+  const bool loader = wave < static_cast<uint32_t>(L);
+  const uint32_t lane16 = lane * 16;
+  auto item_at = [&](uint32_t i, uint32_t& o, uint32_t& x0) {
+    const uint32_t w = begin + (i < n_items ? i : 0);
+    o = to_sgpr(w / p.tiles);
+    x0 = (w - o * p.tiles) * kSlot;
+  };
+  auto issue = [&](uint32_t i, int j, uint32_t ri) {
+    if (!loader) return;
+    uint32_t o, x0;
+    item_at(i, o, x0);
+    const v4u_s src = rsrc4(p.objs + static_cast<uint64_t>(o) * p.obj_stride, i < n_items ? ~0u : 0u);
+    const uint32_t part = wave * (kSlot / L);
+    const uint32_t lds = kRing + ri * kSlot + part;
+    const uint32_t soff = to_sgpr(j * p.bs + x0 + part);
+#pragma unroll
+    for (int c = 0; c < kPerLoader; ++c) dma16<NT>(src, lane16, soff + 1024 * c, lds + 1024 * c);
+  };
+#pragma unroll
+  for (int t = 0; t < R - 1; ++t) issue(t / K, t % K, t);
+  uint32_t ring = 0;
+  uint32_t o0, x00;
+  item_at(0, o0, x00);
+  uint32_t run0 = x00 / kTile;  // first 4 KiB tile of the current run
+  uint32_t acc[NR];
+#pragma unroll
+  for (int q = 0; q < NR; ++q) acc[q] = 0;
+#pragma clang loop unroll(disable)
+  for (uint32_t i = 0; i < n_items; ++i) {
+    uint32_t o, x0;
+    item_at(i, o, x0);
+    const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
+    Rsrc dat;
+    if constexpr (DATA) dat = rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride);
+    typename F::Acc s;
+    F::zero(s);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (loader) wait_vm<kPerLoader * (R - 2)>();
+      ring_barrier();
+      const uint32_t rn = ring == 0 ? R - 1 : ring - 1;
+      issue(i + (j + R - 1) / K, (j + R - 1) % K, rn);
+      const v4u xin = *lds_v4(kRing + ring * kSlot + wave * 1024 + lane16);
+      const uint4 x = make_uint4(xin.x, xin.y, xin.z, xin.w);
+      F::template mac<true>(F::kb(0), j * F::kTableBytes, x, s);
+      if constexpr (DATA)
+        buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x0 + wave * 1024, x);
+      ring = ring + 1 == R ? 0 : ring + 1;
+    }
+    F::pin(s);
+    const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x0 + wave * 1024;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      const uint4 v = F::row(s, q);
+      buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, v);
+      acc[q] = crcdev::zmap(acc[q], base + kCrcZ16384) ^ crcdev::raw16(v, base);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    uint32_t on, xn;
+    item_at(i + 1, on, xn);
+    if (i + 1 == n_items || on != o) {  // the run ends: object boundary or the block's last item
+      const uint32_t lev = base + kCrcLevel;
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        uint32_t a = acc[q];
+#pragma unroll
+        for (int l = 0; l < 6; ++l) {
+          const uint32_t other = __shfl_down(a, 1u << l, 64);
+          a = crcdev::zmap(a, lev + 512u * l) ^ other;
+        }
+        if (lane == 0)
+          *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+              static_cast<uintptr_t>(red + 4 * (wave * 4 + q))) = a;
+        acc[q] = 0;
+      }
+      __syncthreads();
+      if (threadIdx.x < static_cast<uint32_t>(NR)) {
+        // waves 2v, 2v+1 (1 KiB apart) -> pairs -> quads -> 8s -> all 16
+        const uint32_t q = threadIdx.x;
+        uint32_t r8[8];
+#pragma unroll
+        for (int v = 0; v < 8; ++v)
+          r8[v] = crcdev::zmap(crcdev::lds32(red + 4 * (8 * v + q)), lev + 512u * 6) ^
+                  crcdev::lds32(red + 4 * (8 * v + 4 + q));
+        uint32_t r4[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) r4[v] = crcdev::zmap(r8[2 * v], lev + 512u * 7) ^ r8[2 * v + 1];
+        const uint32_t a = crcdev::zmap(r4[0], base + kCrcZ4096) ^ r4[1];
+        const uint32_t b = crcdev::zmap(r4[2], base + kCrcZ4096) ^ r4[3];
+        crc_part_at(p, o, run0)[q] = crcdev::zmap(a, base + kCrcZ8192) ^ b;
+      }
+      __syncthreads();
+      run0 = 0;  // the next run starts at its object's first tile
+    }
+  }
+  if (loader) wait_vm<0>();  // no DMA may land in LDS after the block ends
 }
 
 // Data fragments (optional output of encode): the k padded object slices
@@ -1574,7 +1711,7 @@ template <class F, int K, int MODE>
 __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t e, Slots& st,
                                                  const TablePre<F, K>& pre) {
   const uint32_t o = e / p.edge_tiles;
-  const uint32_t tail0 = p.tiles * kTile;
+  const uint32_t tail0 = p.tiles * p.tile_ch * kTile;
   const DescU d = load_desc(p, o);
   const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
   const uint32_t t = tail0 + (e - o * p.edge_tiles) * kTile + threadIdx.x * 16;
@@ -1663,6 +1800,169 @@ __global__ void __launch_bounds__(kThreadsPerBlock) decode_edge_kernel(DecodePar
   Slots st{0xFFFFFFFFu, 1u};
   TablePre<F, K> pre;
   decode_edges<F, K, MODE>(p, blockIdx.x, gridDim.x, st, pre);
+}
+
+// ---------------- decode, loader / consumer split ----------------
+//
+// decode_dma_kernel: the decode pass (MODE kDecode) in the shape of
+// encode_dma_kernel.  An item is W KiB of payload positions of one object;
+// the L loader waves DMA input j of it -- the payload of fragment
+// d.in_idx(j) -- into an R-slot LDS ring, and every wave takes the products
+// of its 1 KiB from LDS, stores a present data input to its object slice at
+// once (kDrop otherwise, as decode_interior) and the rebuilt rows at the
+// item's end.  Table sets live in two LDS slots: the consumer waves (waves
+// >= L, so the loaders' vmcnt carries only DMAs and stores) fetch the set of
+// item i + 1 into registers during item i - 1 and write it to the free slot
+// right after item i's first barrier; the ring's next barrier publishes it.
+// vmcnt: a loader issues, per slot, kPerLoader DMAs then one store (the
+// prologue adds a zero-record store per slot to keep that shape), so slot t
+// has landed when at most 1 + (R - 2) * (kPerLoader + 1) of its operations
+// are younger -- the rows' stores at an item's end only make it conservative.
+template <class F, int K>
+struct TableRegs {
+  static constexpr int kChunks = K * F::kTableBytes / 16;
+  uint4 v[(kChunks + 255) / 256];  // enough for >= 256 fetching threads
+};
+
+template <class F, int K, int R, bool NT, int L = 4, int W = 16>
+__global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
+  static_assert(R >= 2 && R <= K + 1, "ring of 2 .. K + 1 slots");
+  static_assert(L == 2 || L == 4 || L == 8, "loader waves");
+  static_assert((W - L) * 64 >= 256, "at least 256 table-fetching threads");
+  constexpr uint32_t kSlot = 1024u * W;
+  constexpr int kPerLoader = W / L;
+  constexpr uint32_t kTab = table_slot_bytes(K, F::kW);
+  constexpr uint32_t kRing = 2 * kTab;
+  constexpr int kChunks = TableRegs<F, K>::kChunks;
+  constexpr int kFetchers = (W - L) * 64;
+  constexpr int kPerFetcher = (kChunks + kFetchers - 1) / kFetchers;
+  static_assert(kPerFetcher <= static_cast<int>(sizeof(TableRegs<F, K>::v) / 16), "table registers");
+  const uint32_t wave = wave_in_block();
+  if (blockIdx.x < p.edge_blocks) {  // edge items: 256 threads, the stream kernel's code
+    if (threadIdx.x >= kThreadsPerBlock) return;
+    Slots st{0xFFFFFFFFu, 1u};
+    TablePre<F, K> pre;
+    decode_edges<F, K, kDecode>(p, blockIdx.x, p.edge_blocks, st, pre);
+    return;
+  }
+  const ItemRange rg = item_range(p.n_obj * p.tiles, p.xcd_split, interior_block(p.edge_blocks));
+  if (rg.begin >= rg.end) return;  // block-uniform
+  const uint32_t n_items = to_sgpr((rg.end - rg.begin + rg.step - 1) / rg.step);
+  const bool loader = wave < static_cast<uint32_t>(L);
+  const uint32_t lane16 = lane_id() * 16;
+  const uint32_t fetcher = threadIdx.x - L * 64;  // < kFetchers for the consumer waves
+  auto item_at = [&](uint32_t i, uint32_t& o, uint32_t& x0) {
+    const uint32_t w = rg.begin + (i < n_items ? i : 0) * rg.step;
+    o = to_sgpr(w / p.tiles);
+    x0 = (w - o * p.tiles) * kSlot;
+  };
+  auto desc_at = [&](uint32_t i) {
+    uint32_t o, x0;
+    item_at(i, o, x0);
+    return load_desc(p, o);
+  };
+  // loaders: the DMAs of slot (item i with descriptor d, input j) into ring slot ri
+  auto issue = [&](uint32_t i, const DescU& d, int j, uint32_t ri) {
+    if (!loader) return;
+    uint32_t o, x0;
+    item_at(i, o, x0);
+    const v4u_s src = rsrc4(p.frags + static_cast<uint64_t>(o) * p.stripe_stride,
+                            i < n_items ? ~0u : 0u);
+    const uint32_t part = wave * (kSlot / L);
+    const uint32_t lds = kRing + ri * kSlot + part;
+    const uint32_t soff = to_sgpr(in_pos(p, d, j) * p.frag_stride + kHeaderBytes + x0 + part);
+#pragma unroll
+    for (int c = 0; c < kPerLoader; ++c) dma16<NT>(src, lane16, soff + 1024 * c, lds + 1024 * c);
+  };
+  // consumers: table set `table` into registers (zero-record when not needed)
+  TableRegs<F, K> tr;
+  auto fetch = [&](uint32_t table, bool need) {
+    if (loader) return;
+    const Rsrc t = rsrc(p.tables + static_cast<uint64_t>(table) * (K * F::kTableBytes / 4),
+                        need ? K * F::kTableBytes : 0);
+#pragma unroll
+    for (int c = 0; c < kPerFetcher; ++c) tr.v[c] = buf_ld<true>(t, (fetcher + c * kFetchers) * 16, 0);
+  };
+  auto publish = [&](uint32_t slot) {  // tr into table slot `slot` (visible after a barrier)
+    if (loader) return;
+    auto* dst = lds_v4(slot * kTab);
+#pragma unroll
+    for (int c = 0; c < kPerFetcher; ++c) {
+      const uint32_t i = fetcher + c * kFetchers;
+      if (i < static_cast<uint32_t>(kChunks)) {
+        v4u v;
+        v.x = tr.v[c].x;
+        v.y = tr.v[c].y;
+        v.z = tr.v[c].z;
+        v.w = tr.v[c].w;
+        dst[i] = v;
+      }
+    }
+  };
+  DescU d = desc_at(0);
+  DescU dn = desc_at(1);
+  // item 0's set into slot 0 directly; item 1's into registers
+  uint32_t slot = 0, table = d.table();
+  load_tables(p.tables + static_cast<uint64_t>(table) * (K * F::kTableBytes / 4), K * F::kTableBytes, 0);
+  fetch(dn.table(), 1 < n_items && dn.n_out() != 0 && dn.table() != table);
+  __syncthreads();
+  // prologue: slots 0 .. R-2, each followed by a (zero-record) store as in the loop
+  const Rsrc none = rsrc(p.frags, 0);
+#pragma unroll
+  for (int t = 0; t < R - 1; ++t) {
+    issue(t / K, t / K == 0 ? d : dn, t % K, t);
+    if (loader) buf_st(none, lane16, 0, make_uint4(0, 0, 0, 0));
+  }
+  uint32_t ring = 0;
+#pragma clang loop unroll(disable)
+  for (uint32_t i = 0; i < n_items; ++i) {
+    uint32_t o, x0;
+    item_at(i, o, x0);
+    const Rsrc out = rsrc_out(p.out + static_cast<uint64_t>(o) * p.out_stride);
+    const bool copy = d.copy_inputs() != 0;
+    // the slot of item i + 1's set (the one item i - 1 used, or this one again)
+    const bool swap = i + 1 < n_items && dn.n_out() != 0 && dn.table() != table;
+    const uint32_t kb = F::kb(slot * kTab);
+    const DescU d2 = desc_at(i + 2);
+    typename F::Acc s;
+    F::zero(s);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (loader) wait_vm<1 + (R - 2) * (kPerLoader + 1)>();
+      ring_barrier();
+      if (j == 0) {
+        // item i + 1's set into the free slot; item i + 2's into registers
+        // when item i + 1's swap will leave a different set in LDS
+        if (swap) publish(slot ^ 1u);
+        const uint32_t after = swap ? dn.table() : table;
+        fetch(d2.table(), i + 2 < n_items && d2.n_out() != 0 && d2.table() != after);
+      }
+      const uint32_t rn = ring == 0 ? R - 1 : ring - 1;
+      if (j + R - 1 < K)
+        issue(i, d, j + R - 1, rn);
+      else
+        issue(i + 1, dn, j + R - 1 - K, rn);
+      const v4u xin = *lds_v4(kRing + ring * kSlot + wave * 1024 + lane16);
+      const uint4 xv = make_uint4(xin.x, xin.y, xin.z, xin.w);
+      F::mac(kb, j * F::kTableBytes, xv, s);
+      buf_st(out, copy && d.in_idx(j) < static_cast<uint32_t>(K) ? lane16 : kDrop,
+             d.in_idx(j) * p.bs + x0 + wave * 1024, xv);
+      ring = ring + 1 == R ? 0 : ring + 1;
+    }
+    F::pin(s);
+    const uint32_t e = d.n_out();
+#pragma unroll
+    for (int q = 0; q < F::kRows; ++q)
+      buf_st(out, q < static_cast<int>(e) ? lane16 : kDrop, d.out_idx(q) * p.bs + x0 + wave * 1024,
+             F::row(s, q));
+    if (swap) {
+      slot ^= 1u;
+      table = dn.table();
+    }
+    d = dn;
+    dn = d2;
+  }
+  if (loader) wait_vm<0>();  // no DMA may land in LDS after the block ends
 }
 
 // ---------------- launch ----------------
@@ -1876,9 +2176,49 @@ hipError_t launch_encode_crc(EncodeParams p, Kern kern, int per_cu, uint32_t edg
   fp.row0 = p.row0;
   fp.nrows = NR;
   fp.bs = p.bs;
-  fp.tiles = p.tiles;
+  fp.tiles = p.tiles * p.tile_ch;
   fp.edge_tiles = p.edge_tiles;
   fp.grid = static_cast<uint32_t>(grid);
+  fp.tile_ch = p.tile_ch;
+  return launch_crc_finish(fp, stream);
+}
+
+// The inline_crc32 encode in the loader / consumer shape: edge blocks, one
+// 1024-thread block per CU over contiguous item ranges, then the finishing pass.
+template <class F, int K, int NR, bool DATA>
+hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
+  set_tiles(p, last_room(p.bs, p.obj_len, K), 4);
+  const auto kern = encode_crc_dma_kernel<F, K, NR, 3, true, DATA>;
+  constexpr size_t lds = crc_dma_lds_bytes<F, K, 3>();
+  if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
+  const int cus = device_cus();
+  const uint32_t items = p.n_obj * p.tiles;
+  const uint32_t edge_items = std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u);
+  const uint32_t e = (std::min<uint32_t>(edge_items, static_cast<uint32_t>(cus)) + 7u) & ~7u;
+  uint32_t g = std::min<uint32_t>(static_cast<uint32_t>(cus) & ~7u, std::max(items, 1u));
+  if (g >= 8) g &= ~7u;
+  p.edge_blocks = edge_items ? e : 0;
+  p.fused_edges = 1;
+  p.xcd_split = 0;
+  hipLaunchKernelGGL(kern, dim3(g + p.edge_blocks), dim3(1024), lds, stream, p);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return err;
+  CrcFinishParams fp{};
+  fp.parity = p.parity;
+  fp.frag_stride = p.frag_stride;
+  fp.stripe_stride = p.stripe_stride;
+  fp.part = p.crc_part;
+  fp.maps = p.crc_tables;
+  fp.tables = p.crc_finish_tables;
+  fp.n_obj = p.n_obj;
+  fp.m = p.m;
+  fp.row0 = p.row0;
+  fp.nrows = NR;
+  fp.bs = p.bs;
+  fp.tiles = p.tiles * p.tile_ch;
+  fp.edge_tiles = p.edge_tiles;
+  fp.grid = g;
+  fp.tile_ch = p.tile_ch;
   return launch_crc_finish(fp, stream);
 }
 
@@ -1968,6 +2308,10 @@ hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint3
       if (ring == 3 && lw == 8 && sw == 1 && nw == 16) return launch_encode_dma<F, K, NR, 3, true, 8, 1, 16>(p, stream);
       if (ring == 4 && lw == 4 && sw == 1 && nw == 16) return launch_encode_dma<F, K, NR, 4, true, 4, 1, 16>(p, stream);
       if (ring == 3 && lw == 4 && sw == 2 && nw == 16) return launch_encode_dma<F, K, NR, 3, true, 4, 2, 16>(p, stream);
+      if (ring == 3 && lw == 2 && sw == 1 && nw == 16) return launch_encode_dma<F, K, NR, 3, true, 2, 1, 16>(p, stream);
+      if (ring == 3 && lw == 4 && sw == 1 && nw == 12) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream);
+      if (ring == 4 && lw == 4 && sw == 1 && nw == 12) return launch_encode_dma<F, K, NR, 4, true, 4, 1, 12>(p, stream);
+      if (ring == -3 && lw == 4 && sw == 1 && nw == 16) return launch_encode_dma<F, K, NR, 3, false, 4, 1, 16>(p, stream);
     }
     if (ab_knob("ECAMD_ENC_NOCOMP", 0))  // memory-only probe: WRONG parity
       return ntl ? launch_edges_apart(encode_kernel<F, K, NR, true, false, 1, true>, p, lds, items,
@@ -2014,6 +2358,13 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     if constexpr (F::kRows > kRowsPerPass) {
       return hipErrorInvalidValue;  // the fused CRC runs in four-row passes
     } else {
+      if constexpr (K >= kDmaMinK) {
+        const uint64_t dma_items = static_cast<uint64_t>(std::max<int64_t>(room, 0)) / kDmaItem * p.n_obj;
+        if (dma_items >= static_cast<uint64_t>(device_cus()) &&
+            static_cast<uint64_t>(K) * p.bs + 65536u <= 0xFFFFFFFFull && !ab_knob("ECAMD_CRC_STREAM", 0))
+          return data ? launch_encode_crc_dma<F, K, NR, true>(p, stream)
+                      : launch_encode_crc_dma<F, K, NR, false>(p, stream);
+      }
       return data ? launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR, true>, kEncodePerCu,
                                                 edge_items, stream)
                   : launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR>, kEncodePerCu,
@@ -2060,6 +2411,29 @@ constexpr uint32_t decode_lds_bytes() {
   return 2 * table_slot_bytes(K, F::kW);
 }
 
+// The loader / consumer decode (decode_dma_kernel), launched like
+// launch_encode_dma: items of W KiB, edge items in blocks of their own.
+template <class F, int K, int R, bool NT, int L = 4, int W = 16>
+hipError_t launch_decode_dma(DecodeParams p, hipStream_t stream) {
+  p.tile_ch = W / 4;
+  p.tiles = static_cast<uint32_t>(last_room(p.bs, p.obj_len, K) / (1024 * W));
+  p.edge_tiles = (p.bs + kTile - 1) / kTile - p.tiles * p.tile_ch;
+  const auto kern = decode_dma_kernel<F, K, R, NT, L, W>;
+  constexpr size_t lds = 2 * table_slot_bytes(K, F::kW) + R * 1024 * W;
+  if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
+  const int cus = device_cus();
+  const uint32_t items = p.n_obj * p.tiles;
+  const uint32_t edge_items = p.n_obj * p.edge_tiles;
+  const uint32_t e = (std::min<uint32_t>(edge_items, static_cast<uint32_t>(cus)) + 7u) & ~7u;
+  uint32_t g = std::min<uint32_t>(static_cast<uint32_t>(cus) & ~7u, std::max(items, 1u));
+  if (g >= 8) g &= ~7u;
+  p.edge_blocks = edge_items ? e : 0;
+  p.fused_edges = 1;
+  p.xcd_split = xcd_split_for(static_cast<int>(g), kDecodeXcd);
+  hipLaunchKernelGGL(kern, dim3(g + p.edge_blocks), dim3(W * 64), lds, stream, p);
+  return hipGetLastError();
+}
+
 // A/B builds: the alternative decode launches (see launch_encode_ab).
 template <class F, int K, int MODE>
 hipError_t launch_decode_ab(DecodeParams p, hipStream_t stream, uint32_t edge_items) {
@@ -2081,6 +2455,12 @@ hipError_t launch_decode_ab(DecodeParams p, hipStream_t stream, uint32_t edge_it
     if (ab_knob("ECAMD_DEC_NOCOMP", 0))  // memory-only probe: WRONG objects
       return launch_edges_apart(decode_kernel<F, K, MODE, true>, p, lds, items, edge_items, stream,
                                 per_cu, kDecodeXcd);
+    const int dring = ab_knob("ECAMD_DEC_DMA", 0), dl = ab_knob("ECAMD_DEC_DMA_L", 4);
+    const int dw = ab_knob("ECAMD_DEC_DMA_W", 16);
+    if (dring == 4 && dl == 4 && dw == 16) return launch_decode_dma<F, K, 4, true>(p, stream);
+    if (dring == 3 && dl == 8 && dw == 16) return launch_decode_dma<F, K, 3, true, 8>(p, stream);
+    if (dring == 3 && dl == 4 && dw == 12) return launch_decode_dma<F, K, 3, true, 4, 12>(p, stream);
+    if (dring == -3 && dl == 4 && dw == 16) return launch_decode_dma<F, K, 3, false>(p, stream);
     if (ab_knob("ECAMD_DEC_R3", 0))  // round 3: vector descriptor loads, old prologue
       return launch_edges_apart(decode_kernel<F, K, MODE, false, 0, false>, p, lds, items,
                                 edge_items, stream, per_cu, kDecodeXcd);
@@ -2108,6 +2488,7 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
   } else {
     const int64_t lim = MODE == kReconstruct ? static_cast<int64_t>(p.bs)
                                              : last_room(p.bs, p.obj_len, K);
+    p.tile_ch = 1;
     p.tiles = static_cast<uint32_t>(lim / kTile);
     p.edge_tiles = (p.bs + kTile - 1) / kTile - p.tiles;
     constexpr size_t lds = decode_lds_bytes<F, K>();
@@ -2116,6 +2497,12 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
     if constexpr (kAB) {
       const hipError_t e = launch_decode_ab<F, K, MODE>(p, stream, edge_items);
       if (e != hipErrorNotSupported) return e;
+    }
+    // the loader / consumer decode when the batch has a 16 KiB item per CU
+    if constexpr (MODE == kDecode && K >= kDmaMinK && F::kRows <= kRowsPerPass) {
+      const uint64_t dma_items = static_cast<uint64_t>(std::max<int64_t>(lim, 0)) / kDmaItem * p.n_obj;
+      if (dma_items >= static_cast<uint64_t>(device_cus()) && !ab_knob("ECAMD_DEC_STREAM", 0))
+        return launch_decode_dma<F, K, 3, true>(p, stream);
     }
     p.fused_edges = 1;
     return launch_edges_apart(decode_kernel<F, K, MODE>, p, lds, p.n_obj * p.tiles, edge_items,
