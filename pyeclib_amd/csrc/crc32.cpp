@@ -150,6 +150,7 @@ void build_crc_tables(uint32_t bs, uint32_t steps, CrcTables* out) {
   nibble_tables(zeros(4096), out->z4096);
   for (int l = 0; l < 8; ++l) nibble_tables(zeros(uint64_t(16) << l), out->level[l]);
   nibble_tables(zeros(8192), out->z8192);
+  nibble_tables(zeros(12288), out->z12288);
   nibble_tables(zeros(16384), out->z16384);
   Mat inv;
   const uint64_t pad = uint64_t(steps) * 4096 - bs;

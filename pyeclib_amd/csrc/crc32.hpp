@@ -31,7 +31,8 @@ struct CrcTables {
   uint32_t raw16[32][16];     // raw CRC of a 16-byte chunk, per nibble position
   uint32_t z4096[8][16];      // Z_4096
   uint32_t level[8][8][16];   // Z_{16 * 2^l}, l = 0..7 (lane tree)
-  uint32_t z8192[8][16];      // Z_8192, Z_16384: the 16-KiB-item encode (wave tree, Horner)
+  uint32_t z8192[8][16];      // Z_8192, Z_12288, Z_16384: the loader / consumer encode's
+  uint32_t z12288[8][16];     // wave tree and Horner steps (12 / 16 KiB items)
   uint32_t z16384[8][16];
   uint32_t unshift[8][16];    // Z_pad^-1: drops the zero padding past the payload
   uint32_t t0[256];           // bytewise table (header metadata CRC)

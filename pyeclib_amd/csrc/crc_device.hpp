@@ -56,6 +56,20 @@ __device__ __forceinline__ uint32_t raw16(const uint4& x, uint32_t tab) {
   return a;
 }
 
+// Dword d's share of raw16 (raw16(x) = XOR of raw_dword(x[d], d) over d):
+// 8 nibble lookups, for callers that spread a piece's CRC over time.
+__device__ __forceinline__ uint32_t raw_dword(uint32_t w, int d, uint32_t tab) {
+  const uint32_t lo = (w << 2) & 0x3C3C3C3Cu, hi = (w >> 2) & 0x3C3C3C3Cu;
+  uint32_t a = 0;
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    const uint32_t p = 8 * d + 2 * b;
+    a ^= lds32(tab + 64 * p + byte_of(lo, b)) ^ lds32(tab + 64 * (p + 1) + byte_of(hi, b));
+  }
+  asm volatile("" : "+v"(a));
+  return a;
+}
+
 // zlib crc32 of the 59-byte metadata block of a header held as 16 dwords
 // (bytewise table t0 at LDS byte `t0`).
 __device__ __forceinline__ uint32_t meta_crc(const uint32_t (&h)[16], uint32_t t0) {

@@ -527,10 +527,14 @@ __device__ __forceinline__ uint4 zero_tail(const uint4& v, int64_t n) {
 }
 
 // Whole block copies `bytes` of tables from global memory to LDS byte `dst`.
-__device__ __forceinline__ void load_tables(const uint32_t* src, uint32_t bytes, uint32_t dst) {
+// (threads: how many of the block's first threads take part -- the edge
+// items of the 1024-thread loader / consumer kernels run on 256)
+__device__ __forceinline__ void load_tables(const uint32_t* src, uint32_t bytes, uint32_t dst,
+                                            uint32_t threads = 0) {
   auto* d = lds_v4(dst);
   const v4u* s = reinterpret_cast<const v4u*>(src);
-  for (uint32_t i = threadIdx.x; i < bytes / 16; i += blockDim.x) d[i] = s[i];
+  const uint32_t step = threads ? threads : blockDim.x;
+  for (uint32_t i = threadIdx.x; i < bytes / 16; i += step) d[i] = s[i];
 }
 
 // Bytes of data fragment `idx` at payload offset t that belong to the object.
@@ -1272,28 +1276,49 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
 }
 
 // The parity CRC fused into the loader / consumer encode (encode_dma_kernel's
-// shape, W = 16 waves, 16 KiB items).  Block b streams the contiguous items
+// shape, W waves, W KiB items).  Block b streams the contiguous items
 // [N b / G, N (b + 1) / G) (crc_finish_kernel cuts the runs there), so a
-// thread's consecutive pieces of a parity payload are 16 KiB apart: acc =
-// Z_16384(acc) ^ raw16(piece).  A run's flush joins each wave's 64 lanes with
-// the lane tree (Z_16 .. Z_512) and the 16 waves with Z_1024 .. Z_8192, and
-// stores one raw CRC per row at the run's first 4 KiB tile.  The CRC lookups
-// run in the consumer waves while the loaders keep the ring full.
+// thread's consecutive pieces of a parity payload are W KiB apart: acc =
+// Z_{W KiB}(acc) ^ raw16(piece).  A run's flush joins each wave's 64 lanes
+// with the lane tree (Z_16 .. Z_512) and the W waves with Z_1024 .. Z_8192,
+// and stores one raw CRC per row at the run's first 4 KiB tile.
+// DEFER: an item's CRC steps (per row: the Horner shift, then 4 dwords of
+// raw16 lookups) are spread over the next item's K slots instead of running
+// all at once after its last input -- every wave waits at each slot's barrier,
+// so a burst of lookups there leaves the ring without new loads; the item
+// that ends a run takes its steps at once, before the flush.
 constexpr uint32_t kCrcZ8192 = offsetof(CrcTables, z8192);
+constexpr uint32_t kCrcZ12288 = offsetof(CrcTables, z12288);
 constexpr uint32_t kCrcZ16384 = offsetof(CrcTables, z16384);
-template <class F, int K, int R>
+template <class F, int K, int R, int W = 16>
 __host__ __device__ constexpr uint32_t crc_dma_lds_bytes() {
-  // GF tables, CRC maps, 16 waves x 4 rows of partials, the ring
-  return crc_lds_base<F, K>() + ((kCrcLdsBytes + 16 * 4 * 4 + 255u) & ~255u) + R * 16384u;
+  // GF tables, CRC maps, W waves x 4 rows of partials, the ring
+  return crc_lds_base<F, K>() + ((kCrcLdsBytes + W * 4 * 4 + 255u) & ~255u) + R * 1024u * W;
 }
-template <class F, int K, int NR, int R, bool NT, bool DATA = false>
-__global__ void __launch_bounds__(1024) encode_crc_dma_kernel(EncodeParams p) {
-  constexpr int W = 16, L = 4;
+// CRC step u of a row set: u = 5 q is row q's Horner shift, 5 q + 1 + d its
+// dword d of raw16.
+template <int NR>
+__device__ __forceinline__ void crc_step(int u, uint32_t (&acc)[NR], const uint4 (&rows)[NR],
+                                         uint32_t base, uint32_t zshift) {
+  const int q = u / 5, d = u % 5 - 1;
+  if (d < 0) {
+    acc[q] = crcdev::zmap(acc[q], base + zshift);
+  } else {
+    const uint32_t w = d == 0 ? rows[q].x : d == 1 ? rows[q].y : d == 2 ? rows[q].z : rows[q].w;
+    acc[q] ^= crcdev::raw_dword(w, d, base);
+  }
+}
+template <class F, int K, int NR, int R, bool NT, bool DATA = false, int W = 16, bool DEFER = false>
+__global__ void __launch_bounds__(W * 64) encode_crc_dma_kernel(EncodeParams p) {
+  static_assert(W == 12 || W == 16, "12 or 16 waves");
+  constexpr int L = 4;
   constexpr uint32_t kSlot = 1024u * W;
   constexpr int kPerLoader = W / L;
   constexpr uint32_t base = crc_lds_base<F, K>();
   constexpr uint32_t red = base + kCrcLdsBytes;
-  constexpr uint32_t kRing = crc_dma_lds_bytes<F, K, R>() - R * kSlot;
+  constexpr uint32_t kRing = crc_dma_lds_bytes<F, K, R, W>() - R * kSlot;
+  constexpr uint32_t kZItem = W == 16 ? kCrcZ16384 : kCrcZ12288;
+  constexpr int kSteps = 5 * NR;
   load_tables(p.tables, K * F::kTableBytes, 0);
   load_tables(static_cast<const uint32_t*>(p.crc_tables), kCrcLdsBytes, base);
   __syncthreads();
@@ -1334,8 +1359,13 @@ __global__ void __launch_bounds__(1024) encode_crc_dma_kernel(EncodeParams p) {
   item_at(0, o0, x00);
   uint32_t run0 = x00 / kTile;  // first 4 KiB tile of the current run
   uint32_t acc[NR];
+  uint4 prev[NR];  // DEFER: the previous item's rows, their CRC steps pending
 #pragma unroll
-  for (int q = 0; q < NR; ++q) acc[q] = 0;
+  for (int q = 0; q < NR; ++q) {
+    acc[q] = 0;
+    prev[q] = make_uint4(0, 0, 0, 0);
+  }
+  bool pending = false;
 #pragma clang loop unroll(disable)
   for (uint32_t i = 0; i < n_items; ++i) {
     uint32_t o, x0;
@@ -1356,20 +1386,38 @@ __global__ void __launch_bounds__(1024) encode_crc_dma_kernel(EncodeParams p) {
       F::template mac<true>(F::kb(0), j * F::kTableBytes, x, s);
       if constexpr (DATA)
         buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x0 + wave * 1024, x);
+      if constexpr (DEFER) {
+        if (pending) {  // the previous item's CRC steps [K j / .., K (j + 1) / ..)
+#pragma unroll
+          for (int u = j * kSteps / K; u < (j + 1) * kSteps / K; ++u) crc_step<NR>(u, acc, prev, base, kZItem);
+        }
+      }
       ring = ring + 1 == R ? 0 : ring + 1;
     }
     F::pin(s);
     const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x0 + wave * 1024;
+    uint4 rows[NR];
 #pragma unroll
     for (int q = 0; q < NR; ++q) {
-      const uint4 v = F::row(s, q);
-      buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, v);
-      acc[q] = crcdev::zmap(acc[q], base + kCrcZ16384) ^ crcdev::raw16(v, base);
-      __builtin_amdgcn_sched_barrier(0);
+      rows[q] = F::row(s, q);
+      buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, rows[q]);
     }
     uint32_t on, xn;
     item_at(i + 1, on, xn);
-    if (i + 1 == n_items || on != o) {  // the run ends: object boundary or the block's last item
+    const bool run_end = i + 1 == n_items || on != o;  // object boundary or the block's last item
+    if (!DEFER || run_end) {
+#pragma unroll
+      for (int q = 0; q < NR; ++q) {
+        acc[q] = crcdev::zmap(acc[q], base + kZItem) ^ crcdev::raw16(rows[q], base);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      pending = false;
+    } else {
+#pragma unroll
+      for (int q = 0; q < NR; ++q) prev[q] = rows[q];
+      pending = true;
+    }
+    if (run_end) {
       const uint32_t lev = base + kCrcLevel;
 #pragma unroll
       for (int q = 0; q < NR; ++q) {
@@ -1386,19 +1434,26 @@ __global__ void __launch_bounds__(1024) encode_crc_dma_kernel(EncodeParams p) {
       }
       __syncthreads();
       if (threadIdx.x < static_cast<uint32_t>(NR)) {
-        // waves 2v, 2v+1 (1 KiB apart) -> pairs -> quads -> 8s -> all 16
+        // waves 2v, 2v+1 (1 KiB apart) -> pairs (2 KiB) -> quads (4 KiB) -> the item
         const uint32_t q = threadIdx.x;
-        uint32_t r8[8];
+        constexpr int kPairs = W / 2, kQuads = W / 4;
+        uint32_t r2[kPairs];
 #pragma unroll
-        for (int v = 0; v < 8; ++v)
-          r8[v] = crcdev::zmap(crcdev::lds32(red + 4 * (8 * v + q)), lev + 512u * 6) ^
+        for (int v = 0; v < kPairs; ++v)
+          r2[v] = crcdev::zmap(crcdev::lds32(red + 4 * (8 * v + q)), lev + 512u * 6) ^
                   crcdev::lds32(red + 4 * (8 * v + 4 + q));
-        uint32_t r4[4];
+        uint32_t r4[kQuads];
 #pragma unroll
-        for (int v = 0; v < 4; ++v) r4[v] = crcdev::zmap(r8[2 * v], lev + 512u * 7) ^ r8[2 * v + 1];
-        const uint32_t a = crcdev::zmap(r4[0], base + kCrcZ4096) ^ r4[1];
-        const uint32_t b = crcdev::zmap(r4[2], base + kCrcZ4096) ^ r4[3];
-        crc_part_at(p, o, run0)[q] = crcdev::zmap(a, base + kCrcZ8192) ^ b;
+        for (int v = 0; v < kQuads; ++v) r4[v] = crcdev::zmap(r2[2 * v], lev + 512u * 7) ^ r2[2 * v + 1];
+        uint32_t all;
+        if constexpr (W == 16) {
+          const uint32_t a = crcdev::zmap(r4[0], base + kCrcZ4096) ^ r4[1];
+          const uint32_t b = crcdev::zmap(r4[2], base + kCrcZ4096) ^ r4[3];
+          all = crcdev::zmap(a, base + kCrcZ8192) ^ b;
+        } else {
+          all = crcdev::zmap(r4[0], base + kCrcZ8192) ^ crcdev::zmap(r4[1], base + kCrcZ4096) ^ r4[2];
+        }
+        crc_part_at(p, o, run0)[q] = all;
       }
       __syncthreads();
       run0 = 0;  // the next run starts at its object's first tile
@@ -1501,7 +1556,7 @@ __device__ __forceinline__ uint32_t ensure_tables(const DecodeParams& p, const D
       }
     } else {
       load_tables(p.tables + static_cast<uint64_t>(d.table()) * (K * F::kTableBytes / 4),
-                  K * F::kTableBytes, base);
+                  K * F::kTableBytes, base, kThreadsPerBlock);
     }
     __syncthreads();
     st.table = d.table();
@@ -2185,11 +2240,11 @@ hipError_t launch_encode_crc(EncodeParams p, Kern kern, int per_cu, uint32_t edg
 
 // The inline_crc32 encode in the loader / consumer shape: edge blocks, one
 // 1024-thread block per CU over contiguous item ranges, then the finishing pass.
-template <class F, int K, int NR, bool DATA>
+template <class F, int K, int NR, bool DATA, int W = 12, bool DEFER = false>
 hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
-  set_tiles(p, last_room(p.bs, p.obj_len, K), 4);
-  const auto kern = encode_crc_dma_kernel<F, K, NR, 3, true, DATA>;
-  constexpr size_t lds = crc_dma_lds_bytes<F, K, 3>();
+  set_tiles(p, last_room(p.bs, p.obj_len, K), W / 4);
+  const auto kern = encode_crc_dma_kernel<F, K, NR, 3, true, DATA, W, DEFER>;
+  constexpr size_t lds = crc_dma_lds_bytes<F, K, 3, W>();
   if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
   const int cus = device_cus();
   const uint32_t items = p.n_obj * p.tiles;
@@ -2200,7 +2255,7 @@ hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
   p.edge_blocks = edge_items ? e : 0;
   p.fused_edges = 1;
   p.xcd_split = 0;
-  hipLaunchKernelGGL(kern, dim3(g + p.edge_blocks), dim3(1024), lds, stream, p);
+  hipLaunchKernelGGL(kern, dim3(g + p.edge_blocks), dim3(W * 64), lds, stream, p);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return err;
   CrcFinishParams fp{};
@@ -2228,8 +2283,11 @@ hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
 // 256 x 4 MiB, profiles/r04e_ab.txt): R = 3, W = 16 (four consumer waves per
 // SIMD, 16 KiB slots), L = 4 loaders 271.5 us against 285.7 for the stream
 // kernel; R = 3 SW = 2 276.4, R = 5 280.6, R = 4 W = 16 274.6, L = 8 273.4.
-// The default path takes it for k >= kDmaMinK when the batch has an item of
-// 16 KiB for every CU (smaller batches keep the stream kernel's 4 KiB items).
+// Then (profiles/r04j_ab.txt): W = 12 (three waves per SIMD, 12 KiB slots)
+// 267.9 against 270.4 at W = 16; L = 2 269.0; R = 4 W = 12 274.5; cached
+// (not nontemporal) DMA loads 270.3.  The default path takes W = 12 for
+// k >= kDmaMinK when the batch has a 16 KiB item for every CU (smaller
+// batches keep the stream kernel's 4 KiB items).
 constexpr int kDmaMinK = 4;
 constexpr uint32_t kDmaItem = 16 * 1024;
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
@@ -2261,6 +2319,18 @@ hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint3
   const int per_cu = ab_knob("ECAMD_ENC_PER_CU", kEncodePerCu);
   if (p.crc_tables != nullptr) {
     const int crc_per_cu = ab_knob("ECAMD_CRC_PER_CU", kEncodePerCu);
+    if constexpr (K == 10 && NR == 4) {
+      const int cw = ab_knob("ECAMD_CRC_DMA_W", 12), defer = ab_knob("ECAMD_CRC_DEFER", 0);
+      if (cw == 16 && !defer)
+        return data ? launch_encode_crc_dma<F, K, NR, true, 16>(p, stream)
+                    : launch_encode_crc_dma<F, K, NR, false, 16>(p, stream);
+      if (cw == 16 && defer)
+        return data ? launch_encode_crc_dma<F, K, NR, true, 16, true>(p, stream)
+                    : launch_encode_crc_dma<F, K, NR, false, 16, true>(p, stream);
+      if (cw == 12 && defer)
+        return data ? launch_encode_crc_dma<F, K, NR, true, 12, true>(p, stream)
+                    : launch_encode_crc_dma<F, K, NR, false, 12, true>(p, stream);
+    }
     if constexpr (K == 10 && NR == 4)
       if (!data && ab_knob("ECAMD_CRC_NTL", 0))
         return launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR, false, true>, crc_per_cu,
@@ -2377,8 +2447,8 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     const uint64_t dma_items = static_cast<uint64_t>(std::max<int64_t>(room, 0)) / kDmaItem * p.n_obj;
     if (dma_items >= static_cast<uint64_t>(device_cus()) &&
         static_cast<uint64_t>(K) * p.bs + 65536u <= 0xFFFFFFFFull && !ab_knob("ECAMD_ENC_STREAM", 0))
-      return data ? launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, true>(p, stream)
-                  : launch_encode_dma<F, K, NR, 3, true, 4, 1, 16>(p, stream);
+      return data ? launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream)
+                  : launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream);
   }
   p.fused_edges = 1;
   const uint32_t items = p.n_obj * p.tiles;
@@ -2413,6 +2483,10 @@ constexpr uint32_t decode_lds_bytes() {
 
 // The loader / consumer decode (decode_dma_kernel), launched like
 // launch_encode_dma: items of W KiB, edge items in blocks of their own.
+// Measured round 4 (tools/ab_bench.py, same process, profiles/r04j_ab.txt):
+// W = 12 384.9 us against 401.0 for the stream kernel; W = 16 401.9 (its 75
+// VGPRs leave no room for the edge blocks beside a 16-wave block; at 12
+// waves both fit), R = 4 404.5, L = 8 401.3, cached DMA loads 402.6.
 template <class F, int K, int R, bool NT, int L = 4, int W = 16>
 hipError_t launch_decode_dma(DecodeParams p, hipStream_t stream) {
   p.tile_ch = W / 4;
@@ -2459,7 +2533,8 @@ hipError_t launch_decode_ab(DecodeParams p, hipStream_t stream, uint32_t edge_it
     const int dw = ab_knob("ECAMD_DEC_DMA_W", 16);
     if (dring == 4 && dl == 4 && dw == 16) return launch_decode_dma<F, K, 4, true>(p, stream);
     if (dring == 3 && dl == 8 && dw == 16) return launch_decode_dma<F, K, 3, true, 8>(p, stream);
-    if (dring == 3 && dl == 4 && dw == 12) return launch_decode_dma<F, K, 3, true, 4, 12>(p, stream);
+    if (dring == 3 && dl == 4 && dw == 16) return launch_decode_dma<F, K, 3, true, 4, 16>(p, stream);
+    if (dring == 4 && dl == 4 && dw == 12) return launch_decode_dma<F, K, 4, true, 4, 12>(p, stream);
     if (dring == -3 && dl == 4 && dw == 16) return launch_decode_dma<F, K, 3, false>(p, stream);
     if (ab_knob("ECAMD_DEC_R3", 0))  // round 3: vector descriptor loads, old prologue
       return launch_edges_apart(decode_kernel<F, K, MODE, false, 0, false>, p, lds, items,
@@ -2502,7 +2577,7 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
     if constexpr (MODE == kDecode && K >= kDmaMinK && F::kRows <= kRowsPerPass) {
       const uint64_t dma_items = static_cast<uint64_t>(std::max<int64_t>(lim, 0)) / kDmaItem * p.n_obj;
       if (dma_items >= static_cast<uint64_t>(device_cus()) && !ab_knob("ECAMD_DEC_STREAM", 0))
-        return launch_decode_dma<F, K, 3, true>(p, stream);
+        return launch_decode_dma<F, K, 3, true, 4, 12>(p, stream);
     }
     p.fused_edges = 1;
     return launch_edges_apart(decode_kernel<F, K, MODE>, p, lds, p.n_obj * p.tiles, edge_items,

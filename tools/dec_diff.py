@@ -43,7 +43,9 @@ def main():
         for s in sorted(set(sl.tolist()))[:4]:
             p = pos[sl == s]
             print(f"   slice {s}: n={len(p)} first {p[:6].tolist()} mod1024 {sorted(set((p % 1024).tolist()))[:12]}"
-                  f" obj%16 {sorted(set(((s * bs + p) % 16).tolist()))}")
+                  f" obj%16 {sorted(set(((s * bs + p) % 16).tolist()))}"
+                  f" range [{int(p.min())}, {int(p.max())}] 16K-items {sorted(set((p // 16384).tolist()))[:12]}"
+                  f" KiB-in-item {sorted(set(((p % 16384) // 1024).tolist()))}")
 
 
 if __name__ == "__main__":
