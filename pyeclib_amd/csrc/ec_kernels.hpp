@@ -84,7 +84,27 @@ struct EncodeParams {
   const void* crc_tables;
   const void* crc_finish_tables;
   uint32_t* crc_part;
+  // full-stripe encode with the CRC: room for the data fragments' run
+  // partials (n_obj * ceil(bs / 4096) * k u32).  The launcher fuses their CRC
+  // when it takes the loader / consumer CRC kernel and then sets the HOST
+  // flag *crc_data_fused = 1; otherwise the caller runs the CRC pass.
+  uint32_t* crc_part_data;
+  uint32_t* crc_data_fused;
 };
+
+// Loader / consumer kernels (ec_kernels_impl.hpp encode_dma_kernel ...):
+// taken for k >= kDmaMinK when a launch has a kDmaItem interior item for
+// every CU and the input offsets j * bs + x fit 32 bits.
+constexpr int kDmaMinK = 4;
+constexpr uint32_t kDmaItem = 16 * 1024;
+inline bool dma_batch(uint32_t k, uint32_t bs, uint64_t obj_len, uint32_t n_obj, int cus) {
+  if (k < static_cast<uint32_t>(kDmaMinK)) return false;
+  if (static_cast<uint64_t>(k) * bs + 65536u > 0xFFFFFFFFull) return false;
+  int64_t room = static_cast<int64_t>(obj_len) - static_cast<int64_t>(k - 1) * bs;
+  if (room > static_cast<int64_t>(bs)) room = bs;
+  if (room < 0) room = 0;
+  return static_cast<uint64_t>(room) / kDmaItem * n_obj >= static_cast<uint64_t>(cus);
+}
 
 // Per-object decode / reconstruct descriptor (device memory).
 struct ObjDesc {

@@ -1286,14 +1286,22 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
 // raw16 lookups) are spread over the next item's K slots instead of running
 // all at once after its last input -- every wave waits at each slot's barrier,
 // so a burst of lookups there leaves the ring without new loads; the item
-// that ends a run takes its steps at once, before the flush.
+// that ends a run takes its steps at once, before the flush.  Measured
+// (tools/ab_bench.py --crc, same process, profiles/r04k_ab_crc.txt): W = 16
+// 336.7 us, W = 12 347.5, deferred steps 338.4 / 349.8, the stream CRC
+// kernel 343.2 (plain encode 266.9 on that box): the default is W = 16.
+// DATA (full stripe): each input chunk is stored to its data fragment from
+// the ring, and its raw CRC joins that fragment's accumulator in the same slot
+// (40 lookups per slot, no burst); the flush joins the k data rows too and
+// stores their run partials in crc_part_data, which the finishing pass turns
+// into the data fragments' header CRCs -- no separate CRC pass re-reads them.
 constexpr uint32_t kCrcZ8192 = offsetof(CrcTables, z8192);
 constexpr uint32_t kCrcZ12288 = offsetof(CrcTables, z12288);
 constexpr uint32_t kCrcZ16384 = offsetof(CrcTables, z16384);
 template <class F, int K, int R, int W = 16>
 __host__ __device__ constexpr uint32_t crc_dma_lds_bytes() {
-  // GF tables, CRC maps, W waves x 4 rows of partials, the ring
-  return crc_lds_base<F, K>() + ((kCrcLdsBytes + W * 4 * 4 + 255u) & ~255u) + R * 1024u * W;
+  // GF tables, CRC maps, W waves x (4 parity + K data rows) of partials, the ring
+  return crc_lds_base<F, K>() + ((kCrcLdsBytes + W * (4 + K) * 4 + 255u) & ~255u) + R * 1024u * W;
 }
 // CRC step u of a row set: u = 5 q is row q's Horner shift, 5 q + 1 + d its
 // dword d of raw16.
@@ -1319,6 +1327,8 @@ __global__ void __launch_bounds__(W * 64) encode_crc_dma_kernel(EncodeParams p) 
   constexpr uint32_t kRing = crc_dma_lds_bytes<F, K, R, W>() - R * kSlot;
   constexpr uint32_t kZItem = W == 16 ? kCrcZ16384 : kCrcZ12288;
   constexpr int kSteps = 5 * NR;
+  constexpr int KD = DATA ? K : 0;  // data-fragment CRC rows
+  constexpr uint32_t kRows = 4 + KD;  // partials per wave in `red`
   load_tables(p.tables, K * F::kTableBytes, 0);
   load_tables(static_cast<const uint32_t*>(p.crc_tables), kCrcLdsBytes, base);
   __syncthreads();
@@ -1359,6 +1369,9 @@ __global__ void __launch_bounds__(W * 64) encode_crc_dma_kernel(EncodeParams p) 
   item_at(0, o0, x00);
   uint32_t run0 = x00 / kTile;  // first 4 KiB tile of the current run
   uint32_t acc[NR];
+  uint32_t accd[KD > 0 ? KD : 1];  // data fragments' raw CRCs (DATA)
+#pragma unroll
+  for (int j = 0; j < KD; ++j) accd[j] = 0;
   uint4 prev[NR];  // DEFER: the previous item's rows, their CRC steps pending
 #pragma unroll
   for (int q = 0; q < NR; ++q) {
@@ -1384,8 +1397,10 @@ __global__ void __launch_bounds__(W * 64) encode_crc_dma_kernel(EncodeParams p) 
       const v4u xin = *lds_v4(kRing + ring * kSlot + wave * 1024 + lane16);
       const uint4 x = make_uint4(xin.x, xin.y, xin.z, xin.w);
       F::template mac<true>(F::kb(0), j * F::kTableBytes, x, s);
-      if constexpr (DATA)
+      if constexpr (DATA) {
         buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x0 + wave * 1024, x);
+        accd[j] = crcdev::zmap(accd[j], base + kZItem) ^ crcdev::raw16(x, base);
+      }
       if constexpr (DEFER) {
         if (pending) {  // the previous item's CRC steps [K j / .., K (j + 1) / ..)
 #pragma unroll
@@ -1429,19 +1444,32 @@ __global__ void __launch_bounds__(W * 64) encode_crc_dma_kernel(EncodeParams p) 
         }
         if (lane == 0)
           *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
-              static_cast<uintptr_t>(red + 4 * (wave * 4 + q))) = a;
+              static_cast<uintptr_t>(red + 4 * (wave * kRows + q))) = a;
         acc[q] = 0;
       }
+#pragma unroll
+      for (int j = 0; j < KD; ++j) {
+        uint32_t a = accd[j];
+#pragma unroll
+        for (int l = 0; l < 6; ++l) {
+          const uint32_t other = __shfl_down(a, 1u << l, 64);
+          a = crcdev::zmap(a, lev + 512u * l) ^ other;
+        }
+        if (lane == 0)
+          *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
+              static_cast<uintptr_t>(red + 4 * (wave * kRows + 4 + j))) = a;
+        accd[j] = 0;
+      }
       __syncthreads();
-      if (threadIdx.x < static_cast<uint32_t>(NR)) {
-        // waves 2v, 2v+1 (1 KiB apart) -> pairs (2 KiB) -> quads (4 KiB) -> the item
-        const uint32_t q = threadIdx.x;
+      const uint32_t q = threadIdx.x < static_cast<uint32_t>(NR) ? threadIdx.x : 4 + threadIdx.x - NR;
+      if (threadIdx.x < static_cast<uint32_t>(NR + KD)) {
+        // row q: waves 2v, 2v+1 (1 KiB apart) -> pairs (2 KiB) -> quads (4 KiB) -> the item
         constexpr int kPairs = W / 2, kQuads = W / 4;
         uint32_t r2[kPairs];
 #pragma unroll
         for (int v = 0; v < kPairs; ++v)
-          r2[v] = crcdev::zmap(crcdev::lds32(red + 4 * (8 * v + q)), lev + 512u * 6) ^
-                  crcdev::lds32(red + 4 * (8 * v + 4 + q));
+          r2[v] = crcdev::zmap(crcdev::lds32(red + 4 * (2 * v * kRows + q)), lev + 512u * 6) ^
+                  crcdev::lds32(red + 4 * ((2 * v + 1) * kRows + q));
         uint32_t r4[kQuads];
 #pragma unroll
         for (int v = 0; v < kQuads; ++v) r4[v] = crcdev::zmap(r2[2 * v], lev + 512u * 7) ^ r2[2 * v + 1];
@@ -1453,7 +1481,12 @@ __global__ void __launch_bounds__(W * 64) encode_crc_dma_kernel(EncodeParams p) 
         } else {
           all = crcdev::zmap(r4[0], base + kCrcZ8192) ^ crcdev::zmap(r4[1], base + kCrcZ4096) ^ r4[2];
         }
-        crc_part_at(p, o, run0)[q] = all;
+        if (q < 4) {
+          crc_part_at(p, o, run0)[q] = all;
+        } else {
+          const uint64_t total = p.tiles * p.tile_ch + p.edge_tiles;
+          p.crc_part_data[(static_cast<uint64_t>(o) * total + run0) * K + (q - 4)] = all;
+        }
       }
       __syncthreads();
       run0 = 0;  // the next run starts at its object's first tile
@@ -2242,6 +2275,7 @@ hipError_t launch_encode_crc(EncodeParams p, Kern kern, int per_cu, uint32_t edg
 // 1024-thread block per CU over contiguous item ranges, then the finishing pass.
 template <class F, int K, int NR, bool DATA, int W = 12, bool DEFER = false>
 hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
+  if (DATA && (p.crc_part_data == nullptr || p.crc_data_fused == nullptr)) return hipErrorInvalidValue;
   set_tiles(p, last_room(p.bs, p.obj_len, K), W / 4);
   const auto kern = encode_crc_dma_kernel<F, K, NR, 3, true, DATA, W, DEFER>;
   constexpr size_t lds = crc_dma_lds_bytes<F, K, 3, W>();
@@ -2274,7 +2308,15 @@ hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
   fp.edge_tiles = p.edge_tiles;
   fp.grid = g;
   fp.tile_ch = p.tile_ch;
-  return launch_crc_finish(fp, stream);
+  if ((err = launch_crc_finish(fp, stream)) != hipSuccess || !DATA) return err;
+  // the data fragments' headers from their run partials
+  fp.parity = p.data;
+  fp.part = p.crc_part_data;
+  fp.m = K;
+  fp.row0 = 0;
+  fp.nrows = K;
+  if ((err = launch_crc_finish(fp, stream)) == hipSuccess) *p.crc_data_fused = 1;
+  return err;
 }
 
 // The loader / consumer encode (encode_dma_kernel): one W * 64-thread block
@@ -2288,8 +2330,6 @@ hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
 // (not nontemporal) DMA loads 270.3.  The default path takes W = 12 for
 // k >= kDmaMinK when the batch has a 16 KiB item for every CU (smaller
 // batches keep the stream kernel's 4 KiB items).
-constexpr int kDmaMinK = 4;
-constexpr uint32_t kDmaItem = 16 * 1024;
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
           bool DATA = false>
 hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream) {
@@ -2320,10 +2360,10 @@ hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint3
   if (p.crc_tables != nullptr) {
     const int crc_per_cu = ab_knob("ECAMD_CRC_PER_CU", kEncodePerCu);
     if constexpr (K == 10 && NR == 4) {
-      const int cw = ab_knob("ECAMD_CRC_DMA_W", 12), defer = ab_knob("ECAMD_CRC_DEFER", 0);
-      if (cw == 16 && !defer)
-        return data ? launch_encode_crc_dma<F, K, NR, true, 16>(p, stream)
-                    : launch_encode_crc_dma<F, K, NR, false, 16>(p, stream);
+      const int cw = ab_knob("ECAMD_CRC_DMA_W", 16), defer = ab_knob("ECAMD_CRC_DEFER", 0);
+      if (cw == 12 && !defer)
+        return data ? launch_encode_crc_dma<F, K, NR, true, 12>(p, stream)
+                    : launch_encode_crc_dma<F, K, NR, false, 12>(p, stream);
       if (cw == 16 && defer)
         return data ? launch_encode_crc_dma<F, K, NR, true, 16, true>(p, stream)
                     : launch_encode_crc_dma<F, K, NR, false, 16, true>(p, stream);
@@ -2429,11 +2469,9 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
       return hipErrorInvalidValue;  // the fused CRC runs in four-row passes
     } else {
       if constexpr (K >= kDmaMinK) {
-        const uint64_t dma_items = static_cast<uint64_t>(std::max<int64_t>(room, 0)) / kDmaItem * p.n_obj;
-        if (dma_items >= static_cast<uint64_t>(device_cus()) &&
-            static_cast<uint64_t>(K) * p.bs + 65536u <= 0xFFFFFFFFull && !ab_knob("ECAMD_CRC_STREAM", 0))
-          return data ? launch_encode_crc_dma<F, K, NR, true>(p, stream)
-                      : launch_encode_crc_dma<F, K, NR, false>(p, stream);
+        if (dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) && !ab_knob("ECAMD_CRC_STREAM", 0))
+          return data ? launch_encode_crc_dma<F, K, NR, true, 16>(p, stream)
+                      : launch_encode_crc_dma<F, K, NR, false, 16>(p, stream);
       }
       return data ? launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR, true>, kEncodePerCu,
                                                 edge_items, stream)
@@ -2444,9 +2482,7 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   // the loader / consumer encode (encode_dma_kernel) for k >= kDmaMinK; its
   // input offsets j * bs + x are 32-bit
   if constexpr (F::kRows <= kRowsPerPass && K >= kDmaMinK) {
-    const uint64_t dma_items = static_cast<uint64_t>(std::max<int64_t>(room, 0)) / kDmaItem * p.n_obj;
-    if (dma_items >= static_cast<uint64_t>(device_cus()) &&
-        static_cast<uint64_t>(K) * p.bs + 65536u <= 0xFFFFFFFFull && !ab_knob("ECAMD_ENC_STREAM", 0))
+    if (dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) && !ab_knob("ECAMD_ENC_STREAM", 0))
       return data ? launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream)
                   : launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream);
   }
@@ -2575,8 +2611,7 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
     }
     // the loader / consumer decode when the batch has a 16 KiB item per CU
     if constexpr (MODE == kDecode && K >= kDmaMinK && F::kRows <= kRowsPerPass) {
-      const uint64_t dma_items = static_cast<uint64_t>(std::max<int64_t>(lim, 0)) / kDmaItem * p.n_obj;
-      if (dma_items >= static_cast<uint64_t>(device_cus()) && !ab_knob("ECAMD_DEC_STREAM", 0))
+      if (dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) && !ab_knob("ECAMD_DEC_STREAM", 0))
         return launch_decode_dma<F, K, 3, true, 4, 12>(p, stream);
     }
     p.fused_edges = 1;

@@ -1202,12 +1202,14 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
       (void)upload_done(I, u, stream);
       return hip_errno(te);
     }
-    const size_t part_bytes = static_cast<size_t>(n_obj) * total * m * sizeof(uint32_t);
+    // parity partials, then room for the data fragments' (full stripe)
+    const size_t part_bytes = static_cast<size_t>(n_obj) * total * (m + (data ? k : 0)) * sizeof(uint32_t);
     if ((e = crc_part_for(I, stream, part_bytes, &crc_part)) != hipSuccess) {
       (void)upload_done(I, u, stream);
       return hip_errno(e);
     }
   }
+  uint32_t data_crc_fused = 0;  // set by the launcher (EncodeParams::crc_data_fused)
   // one eight-row pass for 4 < m <= 8 (the fused CRC keeps four-row passes)
   const bool wide = I.wide && !fused_crc;
   const uint32_t passes = wide ? 1 : I.passes;
@@ -1216,6 +1218,10 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
     P.crc_tables = crc_maps;
     P.crc_finish_tables = crc_fin;
     P.crc_part = crc_part;
+    if (fused_crc && data) {
+      P.crc_part_data = crc_part + static_cast<size_t>(n_obj) * ((bs + 4095) / 4096) * m;
+      P.crc_data_fused = &data_crc_fused;
+    }
     P.objs = objs;
     P.obj_stride = obj_stride;
     P.obj_len = obj_len;
@@ -1246,7 +1252,8 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
   if ((e = upload_done(I, u, stream)) != hipSuccess) return hip_errno(e);
   if (headers && I.ct == CHKSUM_CRC32) {
     int rc = fused_crc ? 0 : run_crc(I, parity, frag_stride, stripe_stride, m, n_obj, bs, stream);
-    if (rc == 0 && data) rc = run_crc(I, data, frag_stride, stripe_stride, k, n_obj, bs, stream);
+    if (rc == 0 && data && !data_crc_fused)
+      rc = run_crc(I, data, frag_stride, stripe_stride, k, n_obj, bs, stream);
     if (rc < 0) return rc;
   }
   return 0;
