@@ -1013,7 +1013,7 @@ __host__ __device__ constexpr uint32_t dma_lds_bytes() {
 // W: waves per block (8 = 2 per SIMD, 16 = 4 per SIMD).  DATA: the consumers
 // also store each slot they read from LDS into its data fragment.
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
-          bool DATA = false>
+          bool DATA = false, bool NOCOMP = false>
 __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   static_assert(R >= 2 && R <= K + 1, "ring of 2 .. K + 1 slots");
   static_assert(L == 2 || L == 4 || L == 8 || L == 16, "loader waves");
@@ -1083,7 +1083,12 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
       for (int c = 0; c < SW; ++c) {
         const v4u xin = *lds_v4(kRing + ring * kSlot + (wave * SW + c) * 1024 + lane16);
         const uint4 x = make_uint4(xin.x, xin.y, xin.z, xin.w);
-        F::template mac<true>(F::kb(0), j * F::kTableBytes, x, s[c]);
+        if constexpr (NOCOMP) {  // memory-only probe (A/B builds): WRONG parity
+          uint32_t* a = reinterpret_cast<uint32_t*>(&s[c]);
+          a[0] ^= x.x;
+        } else {
+          F::template mac<true>(F::kb(0), j * F::kTableBytes, x, s[c]);
+        }
         if constexpr (DATA)
           buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x0 + (wave * SW + c) * 1024, x);
       }
@@ -1912,7 +1917,9 @@ struct TableRegs {
   uint4 v[(kChunks + 255) / 256];  // enough for >= 256 fetching threads
 };
 
-template <class F, int K, int R, bool NT, int L = 4, int W = 16>
+// PROBE (A/B builds, WRONG objects): 1 = XORs instead of the lookups
+// (memory-only), 2 = object stores moved down to 16-B alignment.
+template <class F, int K, int R, bool NT, int L = 4, int W = 16, int PROBE = 0>
 __global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
   static_assert(R >= 2 && R <= K + 1, "ring of 2 .. K + 1 slots");
   static_assert(L == 2 || L == 4 || L == 8, "loader waves");
@@ -2032,17 +2039,24 @@ __global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
         issue(i + 1, dn, j + R - 1 - K, rn);
       const v4u xin = *lds_v4(kRing + ring * kSlot + wave * 1024 + lane16);
       const uint4 xv = make_uint4(xin.x, xin.y, xin.z, xin.w);
-      F::mac(kb, j * F::kTableBytes, xv, s);
+      if constexpr (PROBE == 1) {
+        uint32_t* a = reinterpret_cast<uint32_t*>(&s);
+        a[0] ^= xv.x;
+      } else {
+        F::mac(kb, j * F::kTableBytes, xv, s);
+      }
+      const uint32_t slice = PROBE == 2 ? (d.in_idx(j) * p.bs) & ~15u : d.in_idx(j) * p.bs;
       buf_st(out, copy && d.in_idx(j) < static_cast<uint32_t>(K) ? lane16 : kDrop,
-             d.in_idx(j) * p.bs + x0 + wave * 1024, xv);
+             slice + x0 + wave * 1024, xv);
       ring = ring + 1 == R ? 0 : ring + 1;
     }
     F::pin(s);
     const uint32_t e = d.n_out();
 #pragma unroll
-    for (int q = 0; q < F::kRows; ++q)
-      buf_st(out, q < static_cast<int>(e) ? lane16 : kDrop, d.out_idx(q) * p.bs + x0 + wave * 1024,
-             F::row(s, q));
+    for (int q = 0; q < F::kRows; ++q) {
+      const uint32_t slice = PROBE == 2 ? (d.out_idx(q) * p.bs) & ~15u : d.out_idx(q) * p.bs;
+      buf_st(out, q < static_cast<int>(e) ? lane16 : kDrop, slice + x0 + wave * 1024, F::row(s, q));
+    }
     if (swap) {
       slot ^= 1u;
       table = dn.table();
@@ -2331,10 +2345,10 @@ hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
 // k >= kDmaMinK when the batch has a 16 KiB item for every CU (smaller
 // batches keep the stream kernel's 4 KiB items).
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
-          bool DATA = false>
+          bool DATA = false, bool NOCOMP = false>
 hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream) {
   set_tiles(p, last_room(p.bs, p.obj_len, K), 1024u * W * SW / kTile);
-  const auto kern = encode_dma_kernel<F, K, NR, R, NT, L, SW, W, DATA>;
+  const auto kern = encode_dma_kernel<F, K, NR, R, NT, L, SW, W, DATA, NOCOMP>;
   constexpr size_t lds = dma_lds_bytes<F, K, R, SW, W>();
   if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
   const int cus = device_cus();
@@ -2422,6 +2436,8 @@ hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint3
       if (ring == 3 && lw == 4 && sw == 1 && nw == 12) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream);
       if (ring == 4 && lw == 4 && sw == 1 && nw == 12) return launch_encode_dma<F, K, NR, 4, true, 4, 1, 12>(p, stream);
       if (ring == -3 && lw == 4 && sw == 1 && nw == 16) return launch_encode_dma<F, K, NR, 3, false, 4, 1, 16>(p, stream);
+      if (ab_knob("ECAMD_ENC_DMA_NOCOMP", 0))
+        return launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, true>(p, stream);
     }
     if (ab_knob("ECAMD_ENC_NOCOMP", 0))  // memory-only probe: WRONG parity
       return ntl ? launch_edges_apart(encode_kernel<F, K, NR, true, false, 1, true>, p, lds, items,
@@ -2523,19 +2539,19 @@ constexpr uint32_t decode_lds_bytes() {
 // W = 12 384.9 us against 401.0 for the stream kernel; W = 16 401.9 (its 75
 // VGPRs leave no room for the edge blocks beside a 16-wave block; at 12
 // waves both fit), R = 4 404.5, L = 8 401.3, cached DMA loads 402.6.
-template <class F, int K, int R, bool NT, int L = 4, int W = 16>
+template <class F, int K, int R, bool NT, int L = 4, int W = 16, int PROBE = 0, int PER_CU = 1>
 hipError_t launch_decode_dma(DecodeParams p, hipStream_t stream) {
   p.tile_ch = W / 4;
   p.tiles = static_cast<uint32_t>(last_room(p.bs, p.obj_len, K) / (1024 * W));
   p.edge_tiles = (p.bs + kTile - 1) / kTile - p.tiles * p.tile_ch;
-  const auto kern = decode_dma_kernel<F, K, R, NT, L, W>;
+  const auto kern = decode_dma_kernel<F, K, R, NT, L, W, PROBE>;
   constexpr size_t lds = 2 * table_slot_bytes(K, F::kW) + R * 1024 * W;
   if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
   const int cus = device_cus();
   const uint32_t items = p.n_obj * p.tiles;
   const uint32_t edge_items = p.n_obj * p.edge_tiles;
   const uint32_t e = (std::min<uint32_t>(edge_items, static_cast<uint32_t>(cus)) + 7u) & ~7u;
-  uint32_t g = std::min<uint32_t>(static_cast<uint32_t>(cus) & ~7u, std::max(items, 1u));
+  uint32_t g = std::min<uint32_t>((static_cast<uint32_t>(cus) * PER_CU) & ~7u, std::max(items, 1u));
   if (g >= 8) g &= ~7u;
   p.edge_blocks = edge_items ? e : 0;
   p.fused_edges = 1;
@@ -2570,6 +2586,10 @@ hipError_t launch_decode_ab(DecodeParams p, hipStream_t stream, uint32_t edge_it
     if (dring == 4 && dl == 4 && dw == 16) return launch_decode_dma<F, K, 4, true>(p, stream);
     if (dring == 3 && dl == 8 && dw == 16) return launch_decode_dma<F, K, 3, true, 8>(p, stream);
     if (dring == 3 && dl == 4 && dw == 16) return launch_decode_dma<F, K, 3, true, 4, 16>(p, stream);
+    if (dring == 3 && dl == 2 && dw == 12) return launch_decode_dma<F, K, 3, true, 2, 12>(p, stream);
+    if (dring == 3 && dl == 4 && dw == 8) return launch_decode_dma<F, K, 3, true, 4, 8, 0, 2>(p, stream);
+    if (ab_knob("ECAMD_DEC_DMA_NOCOMP", 0) == 1) return launch_decode_dma<F, K, 3, true, 4, 12, 1>(p, stream);
+    if (ab_knob("ECAMD_DEC_DMA_NOCOMP", 0) == 2) return launch_decode_dma<F, K, 3, true, 4, 12, 2>(p, stream);
     if (dring == 4 && dl == 4 && dw == 12) return launch_decode_dma<F, K, 4, true, 4, 12>(p, stream);
     if (dring == -3 && dl == 4 && dw == 16) return launch_decode_dma<F, K, 3, false>(p, stream);
     if (ab_knob("ECAMD_DEC_R3", 0))  // round 3: vector descriptor loads, old prologue
