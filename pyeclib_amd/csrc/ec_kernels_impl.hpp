@@ -1012,8 +1012,11 @@ __host__ __device__ constexpr uint32_t dma_lds_bytes() {
 
 // W: waves per block (8 = 2 per SIMD, 16 = 4 per SIMD).  DATA: the consumers
 // also store each slot they read from LDS into its data fragment.
+// CONTIG (A/B): each block streams a contiguous range of items (the fused-CRC
+// kernel's order) instead of the XCD-split grid stride.  RUNS (A/B): runs of
+// RUNS consecutive items dealt to the blocks grid-stride.
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
-          bool DATA = false, bool NOCOMP = false>
+          bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0>
 __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   static_assert(R >= 2 && R <= K + 1, "ring of 2 .. K + 1 slots");
   static_assert(L == 2 || L == 4 || L == 8 || L == 16, "loader waves");
@@ -1031,15 +1034,34 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   for (uint32_t i = threadIdx.x; i < K * F::kTableBytes / 16; i += W * 64)
     lds_v4(0)[i] = reinterpret_cast<const v4u*>(p.tables)[i];
   __syncthreads();
-  const ItemRange rg = item_range(p.n_obj * p.tiles, p.xcd_split, interior_block(p.edge_blocks));
-  if (rg.begin >= rg.end) return;  // block-uniform
-  const uint32_t n_items = to_sgpr((rg.end - rg.begin + rg.step - 1) / rg.step);
+  ItemRange rg = item_range(p.n_obj * p.tiles, p.xcd_split, interior_block(p.edge_blocks));
+  if constexpr (CONTIG) {
+    const uint64_t nall = static_cast<uint64_t>(p.n_obj) * p.tiles;
+    const IBlock ib = interior_block(p.edge_blocks);
+    rg = {static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nall * ib.b / ib.g))),
+          static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nall * (ib.b + 1) / ib.g))),
+          1u};
+  }
+  uint32_t n_items = 0;
+  const IBlock ibk = interior_block(p.edge_blocks);
+  const uint32_t nall = p.n_obj * p.tiles;
+  const uint32_t runs_total = RUNS ? (nall + RUNS - 1) / RUNS : 0;
+  if constexpr (RUNS > 0) {
+    if (ibk.b >= runs_total) return;  // block-uniform
+    n_items = (runs_total - ibk.b + ibk.g - 1) / ibk.g * RUNS;
+    if ((runs_total - 1 - ibk.b) % ibk.g == 0) n_items -= runs_total * RUNS - nall;
+    n_items = to_sgpr(n_items);
+  } else {
+    if (rg.begin >= rg.end) return;  // block-uniform
+    n_items = to_sgpr((rg.end - rg.begin + rg.step - 1) / rg.step);
+  }
   const bool loader = wave < static_cast<uint32_t>(L);
   const uint32_t lane16 = lane_id() * 16;
   constexpr uint32_t kRing = dma_ring_base<F, K>();
   // item i of this block: object and first payload position
   auto item_at = [&](uint32_t i, uint32_t& o, uint32_t& x0) {
-    const uint32_t w = rg.begin + i * rg.step;
+    const uint32_t w = RUNS ? (ibk.b + ibk.g * (i / (RUNS ? RUNS : 1))) * RUNS + i % (RUNS ? RUNS : 1)
+                            : rg.begin + i * rg.step;
     o = to_sgpr(w / p.tiles);
     x0 = (w - o * p.tiles) * kSlot;
   };
@@ -1897,8 +1919,9 @@ __global__ void __launch_bounds__(kThreadsPerBlock) decode_edge_kernel(DecodePar
 
 // ---------------- decode, loader / consumer split ----------------
 //
-// decode_dma_kernel: the decode pass (MODE kDecode) in the shape of
-// encode_dma_kernel.  An item is W KiB of payload positions of one object;
+// decode_dma_kernel: the decode pass (MODE kDecode) and reconstruct (MODE
+// kReconstruct: row 0 into the fragment payload, no input copies) in the
+// shape of encode_dma_kernel.  An item is W KiB of payload positions of one object;
 // the L loader waves DMA input j of it -- the payload of fragment
 // d.in_idx(j) -- into an R-slot LDS ring, and every wave takes the products
 // of its 1 KiB from LDS, stores a present data input to its object slice at
@@ -1919,8 +1942,10 @@ struct TableRegs {
 
 // PROBE (A/B builds, WRONG objects): 1 = XORs instead of the lookups
 // (memory-only), 2 = object stores moved down to 16-B alignment.
-template <class F, int K, int R, bool NT, int L = 4, int W = 16, int PROBE = 0>
+template <class F, int K, int R, bool NT, int L = 4, int W = 16, int PROBE = 0, int MODE = kDecode>
 __global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
+  static_assert(MODE == kDecode || MODE == kReconstruct, "decode pass or reconstruct");
+  constexpr int S = MODE == kReconstruct ? 0 : 1;  // stores per slot (decode: the input copy)
   static_assert(R >= 2 && R <= K + 1, "ring of 2 .. K + 1 slots");
   static_assert(L == 2 || L == 4 || L == 8, "loader waves");
   static_assert((W - L) * 64 >= 256, "at least 256 table-fetching threads");
@@ -1937,7 +1962,7 @@ __global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
     if (threadIdx.x >= kThreadsPerBlock) return;
     Slots st{0xFFFFFFFFu, 1u};
     TablePre<F, K> pre;
-    decode_edges<F, K, kDecode>(p, blockIdx.x, p.edge_blocks, st, pre);
+    decode_edges<F, K, MODE>(p, blockIdx.x, p.edge_blocks, st, pre);
     return;
   }
   const ItemRange rg = item_range(p.n_obj * p.tiles, p.xcd_split, interior_block(p.edge_blocks));
@@ -2006,7 +2031,7 @@ __global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
 #pragma unroll
   for (int t = 0; t < R - 1; ++t) {
     issue(t / K, t / K == 0 ? d : dn, t % K, t);
-    if (loader) buf_st(none, lane16, 0, make_uint4(0, 0, 0, 0));
+    if (S && loader) buf_st(none, lane16, 0, make_uint4(0, 0, 0, 0));
   }
   uint32_t ring = 0;
 #pragma clang loop unroll(disable)
@@ -2014,7 +2039,7 @@ __global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
     uint32_t o, x0;
     item_at(i, o, x0);
     const Rsrc out = rsrc_out(p.out + static_cast<uint64_t>(o) * p.out_stride);
-    const bool copy = d.copy_inputs() != 0;
+    const bool copy = MODE != kReconstruct && d.copy_inputs() != 0;
     // the slot of item i + 1's set (the one item i - 1 used, or this one again)
     const bool swap = i + 1 < n_items && dn.n_out() != 0 && dn.table() != table;
     const uint32_t kb = F::kb(slot * kTab);
@@ -2023,7 +2048,7 @@ __global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
     F::zero(s);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      if (loader) wait_vm<1 + (R - 2) * (kPerLoader + 1)>();
+      if (loader) wait_vm<S + (R - 2) * (kPerLoader + S)>();
       ring_barrier();
       if (j == 0) {
         // item i + 1's set into the free slot; item i + 2's into registers
@@ -2045,17 +2070,23 @@ __global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
       } else {
         F::mac(kb, j * F::kTableBytes, xv, s);
       }
-      const uint32_t slice = PROBE == 2 ? (d.in_idx(j) * p.bs) & ~15u : d.in_idx(j) * p.bs;
-      buf_st(out, copy && d.in_idx(j) < static_cast<uint32_t>(K) ? lane16 : kDrop,
-             slice + x0 + wave * 1024, xv);
+      if constexpr (MODE != kReconstruct) {
+        const uint32_t slice = PROBE == 2 ? (d.in_idx(j) * p.bs) & ~15u : d.in_idx(j) * p.bs;
+        buf_st(out, copy && d.in_idx(j) < static_cast<uint32_t>(K) ? lane16 : kDrop,
+               slice + x0 + wave * 1024, xv);
+      }
       ring = ring + 1 == R ? 0 : ring + 1;
     }
     F::pin(s);
-    const uint32_t e = d.n_out();
+    if constexpr (MODE == kReconstruct) {
+      buf_st(out, lane16, kHeaderBytes + x0 + wave * 1024, F::row(s, 0));
+    } else {
+      const uint32_t e = d.n_out();
 #pragma unroll
-    for (int q = 0; q < F::kRows; ++q) {
-      const uint32_t slice = PROBE == 2 ? (d.out_idx(q) * p.bs) & ~15u : d.out_idx(q) * p.bs;
-      buf_st(out, q < static_cast<int>(e) ? lane16 : kDrop, slice + x0 + wave * 1024, F::row(s, q));
+      for (int q = 0; q < F::kRows; ++q) {
+        const uint32_t slice = PROBE == 2 ? (d.out_idx(q) * p.bs) & ~15u : d.out_idx(q) * p.bs;
+        buf_st(out, q < static_cast<int>(e) ? lane16 : kDrop, slice + x0 + wave * 1024, F::row(s, q));
+      }
     }
     if (swap) {
       slot ^= 1u;
@@ -2345,10 +2376,10 @@ hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
 // k >= kDmaMinK when the batch has a 16 KiB item for every CU (smaller
 // batches keep the stream kernel's 4 KiB items).
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
-          bool DATA = false, bool NOCOMP = false>
+          bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0>
 hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream) {
   set_tiles(p, last_room(p.bs, p.obj_len, K), 1024u * W * SW / kTile);
-  const auto kern = encode_dma_kernel<F, K, NR, R, NT, L, SW, W, DATA, NOCOMP>;
+  const auto kern = encode_dma_kernel<F, K, NR, R, NT, L, SW, W, DATA, NOCOMP, CONTIG, RUNS>;
   constexpr size_t lds = dma_lds_bytes<F, K, R, SW, W>();
   if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
   const int cus = device_cus();
@@ -2438,6 +2469,14 @@ hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint3
       if (ring == -3 && lw == 4 && sw == 1 && nw == 16) return launch_encode_dma<F, K, NR, 3, false, 4, 1, 16>(p, stream);
       if (ab_knob("ECAMD_ENC_DMA_NOCOMP", 0))
         return launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, true>(p, stream);
+      if (ab_knob("ECAMD_ENC_DMA_CONTIG", 0) == 12)
+        return launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, true>(p, stream);
+      if (ab_knob("ECAMD_ENC_DMA_CONTIG", 0) == 16)
+        return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, false, false, true>(p, stream);
+      const int runs = ab_knob("ECAMD_ENC_DMA_RUNS", 0);
+      if (runs == 2) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, false, false, false, 2>(p, stream);
+      if (runs == 4) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, false, false, false, 4>(p, stream);
+      if (runs == 8) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, false, false, false, 8>(p, stream);
     }
     if (ab_knob("ECAMD_ENC_NOCOMP", 0))  // memory-only probe: WRONG parity
       return ntl ? launch_edges_apart(encode_kernel<F, K, NR, true, false, 1, true>, p, lds, items,
@@ -2539,17 +2578,20 @@ constexpr uint32_t decode_lds_bytes() {
 // W = 12 384.9 us against 401.0 for the stream kernel; W = 16 401.9 (its 75
 // VGPRs leave no room for the edge blocks beside a 16-wave block; at 12
 // waves both fit), R = 4 404.5, L = 8 401.3, cached DMA loads 402.6.
-template <class F, int K, int R, bool NT, int L = 4, int W = 16, int PROBE = 0, int PER_CU = 1>
+template <class F, int K, int R, bool NT, int L = 4, int W = 16, int PROBE = 0, int PER_CU = 1,
+          int MODE = kDecode>
 hipError_t launch_decode_dma(DecodeParams p, hipStream_t stream) {
   p.tile_ch = W / 4;
-  p.tiles = static_cast<uint32_t>(last_room(p.bs, p.obj_len, K) / (1024 * W));
+  const int64_t lim = MODE == kReconstruct ? static_cast<int64_t>(p.bs) : last_room(p.bs, p.obj_len, K);
+  p.tiles = static_cast<uint32_t>(lim / (1024 * W));
   p.edge_tiles = (p.bs + kTile - 1) / kTile - p.tiles * p.tile_ch;
-  const auto kern = decode_dma_kernel<F, K, R, NT, L, W, PROBE>;
+  const auto kern = decode_dma_kernel<F, K, R, NT, L, W, PROBE, MODE>;
   constexpr size_t lds = 2 * table_slot_bytes(K, F::kW) + R * 1024 * W;
   if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
   const int cus = device_cus();
   const uint32_t items = p.n_obj * p.tiles;
-  const uint32_t edge_items = p.n_obj * p.edge_tiles;
+  const uint32_t edge_items =
+      std::max(p.n_obj * p.edge_tiles, MODE == kReconstruct && p.headers ? p.n_obj : 0u);
   const uint32_t e = (std::min<uint32_t>(edge_items, static_cast<uint32_t>(cus)) + 7u) & ~7u;
   uint32_t g = std::min<uint32_t>((static_cast<uint32_t>(cus) * PER_CU) & ~7u, std::max(items, 1u));
   if (g >= 8) g &= ~7u;
@@ -2630,9 +2672,20 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
       if (e != hipErrorNotSupported) return e;
     }
     // the loader / consumer decode when the batch has a 16 KiB item per CU
-    if constexpr (MODE == kDecode && K >= kDmaMinK && F::kRows <= kRowsPerPass) {
-      if (dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) && !ab_knob("ECAMD_DEC_STREAM", 0))
-        return launch_decode_dma<F, K, 3, true, 4, 12>(p, stream);
+    if constexpr (K >= kDmaMinK && F::kRows <= kRowsPerPass) {
+      const int cus = device_cus();
+      if constexpr (MODE == kDecode) {
+        if (dma_batch(K, p.bs, p.obj_len, p.n_obj, cus) && !ab_knob("ECAMD_DEC_STREAM", 0))
+          return launch_decode_dma<F, K, 3, true, 4, 12>(p, stream);
+      } else if constexpr (kAB) {
+        // reconstruct keeps the stream kernel: the loader / consumer form ran
+        // 330.8 us against 259.9 (k=10 m=4 256 x 4 MiB) and 462.9 against
+        // 447.0 (isa_l_rs_cauchy 12+4 128 x 16 MiB; tools/ab_bench.py
+        // --reconstruct, profiles/r04r_ab_reconstruct.txt)
+        if (dma_batch(K, p.bs, static_cast<uint64_t>(K) * p.bs, p.n_obj, cus) &&
+            ab_knob("ECAMD_REC_DMA", 0))
+          return launch_decode_dma<F, K, 3, true, 4, 12, 0, 1, kReconstruct>(p, stream);
+      }
     }
     p.fused_edges = 1;
     return launch_edges_apart(decode_kernel<F, K, MODE>, p, lds, p.n_obj * p.tiles, edge_items,

@@ -94,3 +94,24 @@ def test_dma_inline_crc32(oracle, gpu, ec_type, k, m, n, n_obj):
             assert got[o, i, :80 + bs].tobytes() == want[i], f"obj {o} fragment {i}"
         for p in range(m):
             assert got_par[o, p, :80 + bs].tobytes() == want[k + p], f"obj {o} parity {p}"
+
+
+@pytest.mark.parametrize("ec_type,k,m,n,n_obj", [
+    ("amd_rs_vand", 10, 4, 1 << 20, 48),
+    ("amd_rs_vand", 4, 2, 512 * 1024, 40),
+    ("isa_l_rs_cauchy", 12, 4, (2 << 20) + 5, 32),
+    ("amd_rs_vand", 9, 3, 999999, 64),
+])
+def test_reconstruct_dma_sized_batches(gpu, ec_type, k, m, n, n_obj):
+    """Reconstruct (one random fragment per object, header included) at the
+    batch sizes that take the loader / consumer kernels for encode and decode
+    -- reconstruct itself keeps the stream kernel, which measured faster --
+    every object against the oracle."""
+    import bench
+    from pyeclib_amd import batch
+    from test_gpu_configs import _device_batch
+    codec = batch.BatchCodec(k, m, ec_type=ec_type)
+    assert codec.blocksize(n) // 16384 * n_obj >= MIN_ITEMS, "case must reach the DMA kernels"
+    args, host, masks, dests, gf, g2 = _device_batch(gpu, ec_type, k, m, n, n_obj, "reconstruct")
+    _, _, bad, _ = bench.oracle_pass(args, host, masks, dests, gf, g2, sample=n_obj)
+    assert bad == []

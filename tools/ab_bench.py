@@ -68,6 +68,9 @@ def main():
                          "each decode and the next encode, outside both kernels' events "
                          "(does the encode's alternation cost go away once the decode's "
                          "dirty Infinity-Cache lines are evicted by clean reads?)")
+    ap.add_argument("--reconstruct", action="store_true",
+                    help="the second kernel rebuilds one random fragment per object "
+                         "(header included) instead of decoding; the 'dec' columns time it")
     ap.add_argument("--lib", default=AB_LIB, help="A/B build of the library to load")
     args = ap.parse_args()
 
@@ -105,12 +108,21 @@ def main():
     masks = [full & ~int(sum(1 << int(i) for i in rng.choice(k + m, min(4, m), replace=False)))
              for _ in range(B)]
     out = torch.zeros_like(objs)
+    dests = [int(d) for d in rng.integers(0, k + m, size=B)]
+    rmasks = [full & ~(1 << d) for d in dests]
+    rec = torch.zeros((B, stripes.shape[2]), dtype=torch.uint8, device=dev)
+
+    def second():
+        if args.reconstruct:
+            codec.reconstruct(stripes, n, rmasks, dests, rec)
+        else:
+            codec.decode(stripes, n, masks, out)
     if args.bench_alloc:
         rec = torch.zeros((B, batch.frag_stride(bs)), dtype=torch.uint8, device=dev)  # noqa: F841
     flush = (torch.ones(args.flush_mb << 18, dtype=torch.int32, device=dev)
              if args.flush_mb else None)
     enc_bytes = B * (n + (k + m if args.full_stripe else m) * (bs + 80))
-    dec_bytes = B * (k * bs + n)
+    dec_bytes = B * (k * bs + (bs + 80 if args.reconstruct else n))
 
     variants = [(v, parse_variant(v)) for v in args.variants]
     for _, env in variants:
@@ -127,7 +139,7 @@ def main():
             if args.full_stripe:
                 stripes[:, :k].zero_()
             codec.encode(objs, n, parity=stripes[:, k:], data=data)
-            codec.decode(stripes, n, masks, out)
+            second()
             if args.alt:
                 # bench.py's step: encode, decode, encode, ... each kernel
                 # timed by events around it (each pays for the other's
@@ -138,7 +150,7 @@ def main():
                     ev[3 * i].record()
                     codec.encode(objs, n, parity=stripes[:, k:], data=data)
                     ev[3 * i + 1].record()
-                    codec.decode(stripes, n, masks, out)
+                    second()
                     ev[3 * i + 2].record()
                     if flush is not None:
                         flush.sum()
@@ -155,14 +167,20 @@ def main():
                     codec.encode(objs, n, parity=stripes[:, k:], data=data)
                 ev[1].record()
                 for _ in range(args.reps):
-                    codec.decode(stripes, n, masks, out)
+                    second()
                 ev[2].record()
                 torch.cuda.synchronize()
                 times[name]["enc"].append(ev[0].elapsed_time(ev[1]) / args.reps * 1e3)
                 times[name]["dec"].append(ev[1].elapsed_time(ev[2]) / args.reps * 1e3)
             if rnd == 0 and "NOCOMP" not in name:  # NOCOMP probes compute nothing
                 assert torch.equal(stripes, ref_stripes), f"{name}: stripes differ"
-                assert torch.equal(out[:, :n], objs[:, :n]), f"{name}: decode differs"
+                if args.reconstruct:
+                    idx = torch.tensor(dests, device=dev)
+                    want = stripes[torch.arange(B, device=dev), idx, :80 + bs]
+                    assert torch.equal(rec[:, :80 + bs], want), f"{name}: reconstruct differs"
+                    rec.zero_()
+                else:
+                    assert torch.equal(out[:, :n], objs[:, :n]), f"{name}: decode differs"
                 out.zero_()
     apply({})
 
