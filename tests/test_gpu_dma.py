@@ -36,6 +36,9 @@ def _dma_items(codec, k, n, n_obj):
     ("amd_rs_vand", 28, 4, 2 << 20, 64),
     ("isa_l_rs_cauchy", 12, 4, (2 << 20) + 5, 32),
     ("isa_l_rs_vand", 8, 1, 1 << 20, 32),
+    # many small objects: one 16 KiB item each, plus an edge tile
+    ("amd_rs_vand", 10, 4, 200 * 1024 + 6, 600),
+    ("amd_rs_vand", 30, 2, 2 << 20, 64),
 ])
 def test_dma_encode_decode(gpu, ec_type, k, m, n, n_obj):
     """Full-stripe encode (DATA variant), parity-only encode and decode with
@@ -65,6 +68,7 @@ def test_dma_encode_decode(gpu, ec_type, k, m, n, n_obj):
     ("amd_rs_vand", 8, 6, 1 << 20, 64),        # two parity passes (rows 0-3, 4-5)
     ("isa_l_rs_vand", 10, 4, (1 << 20) + 1, 48),
     ("amd_rs_vand", 5, 3, 777777, 64),
+    ("amd_rs_vand", 10, 4, 200 * 1024 + 6, 600),  # runs end at every object
 ])
 def test_dma_inline_crc32(oracle, gpu, ec_type, k, m, n, n_obj):
     """The fused-CRC loader / consumer encode: every header of a sample of
