@@ -1015,8 +1015,11 @@ __host__ __device__ constexpr uint32_t dma_lds_bytes() {
 // CONTIG (A/B): each block streams a contiguous range of items (the fused-CRC
 // kernel's order) instead of the XCD-split grid stride.  RUNS (A/B): runs of
 // RUNS consecutive items dealt to the blocks grid-stride.
+// COMB (A/B): groups of COMB consecutive blocks share an object, block r of a
+// group taking its tiles r, r + COMB, ... (the order a Horner CRC with a
+// COMB-item stride could use); G / COMB objects in flight.
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
-          bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0>
+          bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0, int COMB = 0>
 __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   static_assert(R >= 2 && R <= K + 1, "ring of 2 .. K + 1 slots");
   static_assert(L == 2 || L == 4 || L == 8 || L == 16, "loader waves");
@@ -1046,7 +1049,13 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   const IBlock ibk = interior_block(p.edge_blocks);
   const uint32_t nall = p.n_obj * p.tiles;
   const uint32_t runs_total = RUNS ? (nall + RUNS - 1) / RUNS : 0;
-  if constexpr (RUNS > 0) {
+  const uint32_t groups = COMB ? ibk.g / COMB : 1, r0 = COMB ? ibk.b % COMB : 0;
+  const uint32_t per_obj = COMB ? (p.tiles > r0 ? (p.tiles - r0 + COMB - 1) / COMB : 0) : 0;
+  if constexpr (COMB > 0) {
+    const uint32_t g0 = ibk.b / COMB;
+    if (per_obj == 0 || g0 >= p.n_obj || ibk.b >= groups * COMB) return;  // block-uniform
+    n_items = to_sgpr((p.n_obj - g0 + groups - 1) / groups * per_obj);
+  } else if constexpr (RUNS > 0) {
     if (ibk.b >= runs_total) return;  // block-uniform
     n_items = (runs_total - ibk.b + ibk.g - 1) / ibk.g * RUNS;
     if ((runs_total - 1 - ibk.b) % ibk.g == 0) n_items -= runs_total * RUNS - nall;
@@ -1060,6 +1069,12 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   constexpr uint32_t kRing = dma_ring_base<F, K>();
   // item i of this block: object and first payload position
   auto item_at = [&](uint32_t i, uint32_t& o, uint32_t& x0) {
+    if constexpr (COMB > 0) {
+      const uint32_t q = i / per_obj, sidx = i - q * per_obj;
+      o = to_sgpr(ibk.b / COMB + q * groups);
+      x0 = (r0 + sidx * COMB) * kSlot;
+      return;
+    }
     const uint32_t w = RUNS ? (ibk.b + ibk.g * (i / (RUNS ? RUNS : 1))) * RUNS + i % (RUNS ? RUNS : 1)
                             : rg.begin + i * rg.step;
     o = to_sgpr(w / p.tiles);
@@ -2376,10 +2391,10 @@ hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
 // k >= kDmaMinK when the batch has a 16 KiB item for every CU (smaller
 // batches keep the stream kernel's 4 KiB items).
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
-          bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0>
+          bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0, int COMB = 0>
 hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream) {
   set_tiles(p, last_room(p.bs, p.obj_len, K), 1024u * W * SW / kTile);
-  const auto kern = encode_dma_kernel<F, K, NR, R, NT, L, SW, W, DATA, NOCOMP, CONTIG, RUNS>;
+  const auto kern = encode_dma_kernel<F, K, NR, R, NT, L, SW, W, DATA, NOCOMP, CONTIG, RUNS, COMB>;
   constexpr size_t lds = dma_lds_bytes<F, K, R, SW, W>();
   if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
   const int cus = device_cus();
@@ -2477,6 +2492,11 @@ hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint3
       if (runs == 2) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, false, false, false, 2>(p, stream);
       if (runs == 4) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, false, false, false, 4>(p, stream);
       if (runs == 8) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, false, false, false, 8>(p, stream);
+      const int comb = ab_knob("ECAMD_ENC_DMA_COMB", 0);
+      if (comb == 4) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, false, false, false, 0, 4>(p, stream);
+      if (comb == 5) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, false, false, false, 0, 5>(p, stream);
+      if (comb == 8) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, false, false, false, 0, 8>(p, stream);
+      if (comb == 16) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, false, false, false, 0, 16>(p, stream);
     }
     if (ab_knob("ECAMD_ENC_NOCOMP", 0))  // memory-only probe: WRONG parity
       return ntl ? launch_edges_apart(encode_kernel<F, K, NR, true, false, 1, true>, p, lds, items,
