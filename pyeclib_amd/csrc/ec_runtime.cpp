@@ -109,10 +109,17 @@ struct Knobs {
   // Round 4 (tools/single_probe.py, profiles/r04e_single_probe.txt): with the
   // parallel host copies, 4 MiB encode 279 -> 215 us through pinned staging.
   size_t single_pinned_max = size_t(64) << 20;  // ECAMD_SINGLE_PINNED_MAX
-  // the kernels read the caller's object (encode) and write the caller's
-  // output (decode) in place, registered with hipHostRegister for the call
-  // (about 3 us for 4 MiB) instead of copying through the staging buffer
-  bool register_caller = true;  // ECAMD_REGISTER_CALLER=0: always copy
+  // Opt-in (ECAMD_REGISTER_CALLER=1): the kernels read the caller's object
+  // (encode) and write the caller's output (decode) in place, registered with
+  // hipHostRegister for the call (about 3 us for 4 MiB) instead of going
+  // through the staging buffer.  Off by default since round 5: a caller's
+  // Python buffer shares its first and last pages with other heap objects,
+  // the runtime pins whole pages, and every GPU fault of round 4 was a torch
+  // pageable copy in a process that had registered such buffers (DESIGN.md
+  // section 6b).  CallerPin keeps the opt-in path safe among this library's
+  // own calls (a process-wide registry: no two live registrations share a
+  // page; unregistration is checked).
+  bool register_caller = false;
   long pool_slots = 0;          // ECAMD_POOL_SLOTS: decode table-set slots (0 = from 32 MiB)
   bool host_staged = false;     // ECAMD_HOST_STAGED: copy-engine host pipeline
   bool host_staged_out = false; // ECAMD_HOST_STAGED_OUT: ... with outputs staged through HBM
@@ -131,7 +138,7 @@ struct Knobs {
     k.host_chunk_mb = static_cast<int>(std::max<long>(1, env_long("ECAMD_HOST_CHUNK_MB", k.host_chunk_mb)));
     k.edge_blocks = env_on("ECAMD_EDGE_BLOCKS", true);
     k.crc_fused = env_on("ECAMD_CRC_FUSED", true);
-    k.register_caller = env_on("ECAMD_REGISTER_CALLER", true);
+    k.register_caller = env_on("ECAMD_REGISTER_CALLER", false);
     return k;
   }
 };
@@ -299,16 +306,24 @@ struct Instance {
   GfMatrix gen;
   std::mutex mu;
   hipStream_t stream = nullptr;
-  // Every stream a launch of this instance has been queued on (a caller's
-  // few streams, the instance's own).  A device buffer the instance rewrites
-  // or frees is read only by launches on these streams, so waiting for them
-  // -- on the GPU where the rewrite is itself queued, on the host where it is
-  // not -- replaces a device-wide synchronisation: other instances' and other
-  // threads' work is never waited for, and every error is returned.
-  // (Streams passed to ecamd_* calls must stay valid while the instance
-  // lives; include/erasurecode_amd.h.)
-  std::vector<hipStream_t> streams;
-  std::vector<hipEvent_t> stream_ev;  // one reusable marker per stream
+  // The end of this instance's work on every stream a launch of it has been
+  // queued on (a caller's few streams, the instance's own): when a call that
+  // launched on stream s returns, the event of s's entry is recorded on s
+  // (CallScope).  A device buffer the instance rewrites or frees is read
+  // only by launches on these streams, so waiting for these events -- on the
+  // GPU where the rewrite is itself queued, on the host where it is not --
+  // replaces a device-wide synchronisation: other instances' and other
+  // threads' work is never waited for, and every error is returned.  A
+  // stream handle is used only during a call on it, so a caller may destroy
+  // its stream once the call returns; entries whose work has completed are
+  // dropped, so a caller taking a new stream per call does not grow the list.
+  struct StreamMark {
+    hipStream_t s;
+    hipEvent_t ev;
+    bool open;      // launched on during the current call: record at its end
+    bool recorded;  // ev marks the end of this instance's work on s
+  };
+  std::vector<StreamMark> marks;
   DevBuf enc_tables;  // passes x k x 64 u64
   // GF(2^16) with 4 < m <= 8: one eight-row table set (k x 1 KiB), so encode
   // reads the object once (ec_kernels_impl.hpp Gf16x8); the four-row passes
@@ -362,34 +377,72 @@ struct Instance {
   // bytes of one table set (k inputs x up to 4 rows)
   size_t table_bytes() const { return static_cast<size_t>(k) * table_bytes_per_input(code.w); }
 
-  // A launch of this instance is about to be queued on s.
+  // A launch of this instance is about to be queued on s (during a call).
   hipError_t note_stream(hipStream_t s) {
-    for (hipStream_t t : streams)
-      if (t == s) return hipSuccess;
+    for (auto& k : marks)
+      if (k.s == s) {
+        k.open = true;
+        return hipSuccess;
+      }
     hipEvent_t ev = nullptr;
     const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e != hipSuccess) return e;
-    streams.push_back(s);
-    stream_ev.push_back(ev);
+    marks.push_back({s, ev, true, false});
     return hipSuccess;
   }
-  // GPU-side: work queued on s from now on runs after everything queued so
-  // far on the instance's other streams (s's own work is ordered already).
+  // End of a call: mark the end of its work on every stream it launched on
+  // (those handles are the call's own, valid now).
+  hipError_t end_call() {
+    hipError_t first = hipSuccess;
+    for (auto& k : marks) {
+      if (!k.open) continue;
+      k.open = false;
+      const hipError_t e = hipEventRecord(k.ev, k.s);
+      k.recorded = e == hipSuccess;
+      if (e != hipSuccess && first == hipSuccess) first = e;
+    }
+    return first;
+  }
+  // Drop the entries (other than s's) whose recorded work has completed.
+  void prune_marks(hipStream_t s) {
+    size_t j = 0;
+    for (size_t i = 0; i < marks.size(); ++i) {
+      StreamMark& k = marks[i];
+      if (k.s != s && !k.open && k.recorded && hipEventQuery(k.ev) == hipSuccess) {
+        (void)hipEventDestroy(k.ev);
+        continue;
+      }
+      marks[j++] = k;
+    }
+    marks.resize(j);
+  }
+  // GPU-side: work queued on s from now on runs after everything this
+  // instance queued so far on its other streams (s's own work is ordered
+  // already): earlier calls' through their end marks, the current call's
+  // (a host pipeline deals chunks over several streams) through a mark
+  // recorded now.
   hipError_t order_after_streams(hipStream_t s) {
-    for (size_t i = 0; i < streams.size(); ++i) {
-      if (streams[i] == s) continue;
-      hipError_t e = hipEventRecord(stream_ev[i], streams[i]);
-      if (e == hipSuccess) e = hipStreamWaitEvent(s, stream_ev[i], 0);
+    prune_marks(s);
+    for (auto& k : marks) {
+      if (k.s == s) continue;
+      if (k.open) {
+        const hipError_t e = hipEventRecord(k.ev, k.s);
+        if (e != hipSuccess) return e;
+        k.recorded = true;
+      }
+      if (!k.recorded) continue;
+      const hipError_t e = hipStreamWaitEvent(s, k.ev, 0);
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
   }
-  // Host-side: wait for everything queued so far on the instance's streams.
+  // Host-side: wait for everything queued so far on the instance's streams
+  // (the current call's launches first get their end marks).
   hipError_t wait_streams() {
-    hipError_t first = hipSuccess;
-    for (size_t i = 0; i < streams.size(); ++i) {
-      hipError_t e = hipEventRecord(stream_ev[i], streams[i]);
-      if (e == hipSuccess) e = hipEventSynchronize(stream_ev[i]);
+    hipError_t first = end_call();
+    for (auto& k : marks) {
+      if (!k.recorded) continue;
+      const hipError_t e = hipEventSynchronize(k.ev);
       if (e != hipSuccess && first == hipSuccess) first = e;
     }
     return first;
@@ -406,7 +459,7 @@ struct Instance {
       }
     for (auto& e : hdone)
       if (e) (void)hipEventDestroy(e);
-    for (auto& e : stream_ev) (void)hipEventDestroy(e);
+    for (auto& k : marks) (void)hipEventDestroy(k.ev);
     if (pool_gen_ev) (void)hipEventDestroy(pool_gen_ev);
     if (pool_ev) {
       (void)hipEventSynchronize(pool_ev);
@@ -466,6 +519,23 @@ struct Instance {
     hipError_t e = hipEventRecord(r->ev, s);
     r->pending = (e == hipSuccess);
     return e;
+  }
+};
+
+// Held by every entry point that may launch (after the instance lock): the
+// call's end marks are recorded however it returns (Instance::end_call).
+// (A/B builds: ECAMD_NO_END_MARK=1 skips them -- single-stream timing only.)
+struct CallScope {
+  Instance& I;
+  explicit CallScope(Instance& i) : I(i) {}
+  CallScope(const CallScope&) = delete;
+  CallScope& operator=(const CallScope&) = delete;
+  ~CallScope() {
+    if (kAB && ab_knob("ECAMD_NO_END_MARK", 0)) {
+      for (auto& k : I.marks) k.open = false;
+      return;
+    }
+    (void)I.end_call();
   }
 };
 
@@ -1464,16 +1534,40 @@ struct PhaseClock {
   }
 };
 
-// A caller's host buffer the kernels use in place for one call: registered
-// (mapped) with hipHostRegister, unregistered when the guard ends -- after
-// the call's stream synchronize.  pin() fails, and the caller copies through
-// the staging buffer instead, when the range cannot be registered (its pages
-// already are, or the range runs into unmapped memory).
+// Page ranges [first, end) that CallerPin holds registered, process-wide.
+// The runtime pins whole pages, so two registrations whose ranges share a
+// page -- neighbouring heap objects, or one buffer passed by two threads --
+// would pin it twice and release it out of order; a registration is refused
+// (the call copies instead) while any page of its range is held.  After a
+// failed unregistration nothing more is registered in the process.
+struct PinRegistry {
+  std::mutex mu;
+  std::map<uintptr_t, uintptr_t> live;
+  bool broken = false;
+};
+PinRegistry* const g_pins = new PinRegistry;  // never destroyed (exit-time calls)
+constexpr uintptr_t kPage = 4096;
+
+// A caller's host buffer the kernels use in place for one call (opt-in,
+// Knobs::register_caller): registered (mapped) with hipHostRegister, and
+// unregistered by unpin() after the call's stream synchronize -- its result
+// is the call's.  pin() fails, and the caller copies through the staging
+// buffer instead, when the range cannot be registered (a page of it is held
+// by another live registration, or the range runs into unmapped memory).
 struct CallerPin {
   void* host = nullptr;
   uint8_t* dev = nullptr;
+  uintptr_t first = 0;
   bool pin(const void* p, size_t n) {
     if (n == 0) return false;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~(kPage - 1);
+    const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + n + kPage - 1) & ~(kPage - 1);
+    PinRegistry& R = *g_pins;
+    std::lock_guard<std::mutex> lk(R.mu);
+    if (R.broken) return false;
+    auto it = R.live.lower_bound(a);
+    if (it != R.live.end() && it->first < b) return false;
+    if (it != R.live.begin() && std::prev(it)->second > a) return false;
     void* h = const_cast<void*>(p);
     if (hipHostRegister(h, n, hipHostRegisterMapped) != hipSuccess) {
       (void)hipGetLastError();
@@ -1482,19 +1576,38 @@ struct CallerPin {
     void* d = nullptr;
     if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || d == nullptr) {
       (void)hipGetLastError();
-      (void)hipHostUnregister(h);
+      if (hipHostUnregister(h) != hipSuccess) {
+        (void)hipGetLastError();
+        R.broken = true;
+        R.live.emplace(a, b);  // still held: keep every later range off it
+      }
       return false;
     }
+    R.live.emplace(a, b);
     host = h;
+    first = a;
     dev = static_cast<uint8_t*>(d);
     return true;
+  }
+  hipError_t unpin() {
+    if (!host) return hipSuccess;
+    PinRegistry& R = *g_pins;
+    std::lock_guard<std::mutex> lk(R.mu);
+    const hipError_t e = hipHostUnregister(host);
+    host = nullptr;
+    dev = nullptr;
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      R.broken = true;  // the range stays in `live`
+      return e;
+    }
+    R.live.erase(first);
+    return hipSuccess;
   }
   CallerPin() = default;
   CallerPin(const CallerPin&) = delete;
   CallerPin& operator=(const CallerPin&) = delete;
-  ~CallerPin() {
-    if (host) (void)hipHostUnregister(host);
-  }
+  ~CallerPin() { (void)unpin(); }  // error paths, after their stream synchronize
 };
 
 // liberasurecode_encode's work for one object, into k + m caller-provided
@@ -1562,6 +1675,7 @@ int encode_into(Instance& I, const char* data, uint64_t len, uint8_t* const* fra
           return hip_errno(e);
         }
     if ((e = hipStreamSynchronize(I.stream)) != hipSuccess) return hip_errno(e);
+    if ((e = src.unpin()) != hipSuccess) return hip_errno(e);
     clk.mark(3);
     if (pin) {
       jobs.clear();
@@ -1589,6 +1703,7 @@ int liberasurecode_encode(int desc, const char* orig_data, uint64_t orig_data_si
   if (!I) return -EBACKENDNOTAVAIL;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
+  CallScope cs(*I);
   const int k = I->k, m = I->m;
   const uint64_t bs = blocksize_of(k, I->code.w, orig_data_size);
   const uint64_t fl = bs + kHeaderBytes;
@@ -1789,6 +1904,7 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
       rc = hip_errno(e);
   clk.mark(1);
   if ((e = hipStreamSynchronize(I.stream)) != hipSuccess && rc == 0) rc = hip_errno(e);
+  if ((e = dst.unpin()) != hipSuccess && rc == 0) rc = hip_errno(e);
   clk.mark(3);
   if (rc == 0 && orig && pin && !direct) host_copy(out, d_obj, orig);
   clk.mark(4);
@@ -1805,6 +1921,7 @@ int liberasurecode_decode(int desc, char** available_fragments, int num_fragment
   if (!I) return -EBACKENDNOTAVAIL;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
+  CallScope cs(*I);
   DecodeIn D;
   int rc = decode_prepare(*I, available_fragments, num_fragments, fragment_len,
                           force_metadata_checks, D);
@@ -1834,6 +1951,7 @@ int liberasurecode_reconstruct_fragment(int desc, char** available_fragments, in
   if (!I) return -EBACKENDNOTAVAIL;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
+  CallScope cs(*I);
   const int k = I->k, m = I->m;
   if (fragment_len < kHeaderBytes) return -EBADHEADER;
   for (int i = 0; i < num_fragments; ++i)
@@ -1967,6 +2085,7 @@ int ecamd_encode_into(int desc, const char* data, uint64_t data_len, char** frag
   if (!I) return -EBACKENDNOTAVAIL;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
+  CallScope cs(*I);
   if (fragment_len != blocksize_of(I->k, I->code.w, data_len) + kHeaderBytes)
     return -EINVALIDPARAMS;
   uint8_t* frags[kMaxFragments];
@@ -1985,6 +2104,7 @@ int ecamd_decode_into(int desc, char** available_fragments, int num_fragments,
   if (!I) return -EBACKENDNOTAVAIL;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
+  CallScope cs(*I);
   DecodeIn D;
   const int rc = decode_prepare(*I, available_fragments, num_fragments, fragment_len,
                                 force_metadata_checks, D);
@@ -2039,6 +2159,7 @@ int ecamd_encode_batch(int desc, const void* d_objs, uint64_t obj_stride, uint64
   if (obj_len == 0) return -EINVALIDPARAMS;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
+  CallScope cs(*I);
   return run_encode(*I, static_cast<const uint8_t*>(d_objs), obj_stride, obj_len, n_obj,
                     static_cast<uint8_t*>(d_parity), static_cast<uint8_t*>(d_data), frag_stride,
                     stripe_stride, true, static_cast<hipStream_t>(stream));
@@ -2054,6 +2175,7 @@ int ecamd_decode_batch(int desc, const void* d_frags, uint64_t frag_stride,
   if (n_obj > 1 && obj_stride < obj_len) return -EINVALIDPARAMS;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
+  CallScope cs(*I);
   DecodeJob J{static_cast<const uint8_t*>(d_frags), frag_stride, stripe_stride, obj_len,
               static_cast<uint8_t*>(d_objs), obj_stride, n_obj, h_avail, nullptr, nullptr};
   return run_decode(*I, J, static_cast<hipStream_t>(stream));
@@ -2070,6 +2192,7 @@ int ecamd_reconstruct_batch(int desc, const void* d_frags, uint64_t frag_stride,
   if (I->ct == CHKSUM_CRC32 && I->legacy_crc) return -EBACKENDNOTSUPP;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
+  CallScope cs(*I);
   const uint64_t bs = blocksize_of(I->k, I->code.w, obj_len);
   std::vector<uint8_t> hdr(static_cast<size_t>(n_obj) * kHeaderBytes);
   for (int o = 0; o < n_obj; ++o) {
@@ -2098,6 +2221,7 @@ int ecamd_encode_host_batch(int desc, const void* h_objs, uint64_t obj_stride, u
   if (frag_stride < kHeaderBytes + round16(bs)) return -EINVALIDPARAMS;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
+  CallScope cs(*I);
   const int m = I->m;
   const uint64_t ps = static_cast<uint64_t>(m) * frag_stride;
   const HostSide H{static_cast<const uint8_t*>(h_objs), obj_stride, obj_len, 0,
@@ -2120,6 +2244,7 @@ int ecamd_decode_host_batch(int desc, const void* h_frags, uint64_t frag_stride,
   if (frag_stride < kHeaderBytes + round16(bs)) return -EINVALIDPARAMS;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
+  CallScope cs(*I);
   const uint64_t gs = static_cast<uint64_t>(I->k) * frag_stride;
   const HostSide H{static_cast<const uint8_t*>(h_frags), gs, gs, 48,
                    static_cast<uint8_t*>(h_objs), obj_stride, obj_len, 0};
@@ -2145,6 +2270,7 @@ int ecamd_reconstruct_host_batch(int desc, const void* h_frags, uint64_t frag_st
     return -EINVALIDPARAMS;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
+  CallScope cs(*I);
   std::vector<uint8_t> hdr(static_cast<size_t>(n_obj) * kHeaderBytes);
   for (int o = 0; o < n_obj; ++o) {
     if (h_dest[o] < 0 || h_dest[o] >= I->k + I->m) return -EINVALIDPARAMS;

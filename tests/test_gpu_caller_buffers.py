@@ -1,0 +1,154 @@
+"""Single-object calls on caller buffers that share pages, from 8 threads.
+
+Round 4's GPU faults were all torch pageable copies in
+processes that had registered callers' Python buffers with hipHostRegister;
+such buffers share their first and last pages with other heap objects.  These
+tests drive the single-object C entry points (ecamd_encode_into /
+ecamd_decode_into, the calls pyeclib_c.c:512-565 and :770-922 make through
+liberasurecode) on slices carved from ONE host array -- so neighbouring calls'
+inputs and outputs share pages by construction, at odd offsets -- from 8
+threads at once (ctypes releases the GIL; the reference's threading contract,
+pyeclib_c.c:1245-1251, test_pyeclib_api.py:192-218), and check:
+  * every fragment and decoded object against the CPU oracle;
+  * guard bytes around every output slice (no store past a caller's buffer);
+  * afterwards, torch pageable host<->device copies of fresh arrays of the
+    sizes that faulted in round 4 (1.0-1.5 MiB) and of the freed arrays'
+    sizes, contents compared.
+"""
+import ctypes
+import os
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+GUARD = 0xA5
+K, M = 10, 4
+
+
+def _carve(total, sizes, gap, align_off):
+    """Offsets of consecutive slices of `sizes` in one array, `gap` guard
+    bytes between them, each starting at an odd offset mod 16 when
+    align_off is set (the caller's bytes are not 16-B aligned)."""
+    offs, at = [], gap
+    for n in sizes:
+        if align_off:
+            at += (7 - at) % 16 or 0
+        offs.append(at)
+        at += n + gap
+    assert at <= total
+    return offs
+
+
+def _run_threads(fn, n):
+    errors = []
+
+    def wrap(i):
+        try:
+            fn(i)
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(f"thread {i}: {e!r}")
+
+    ts = [threading.Thread(target=wrap, args=(i,)) for i in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors
+
+
+def test_threaded_page_sharing_calls(oracle, gpu):
+    import torch
+    from pyeclib_amd import _native
+    lib = _native.lib
+    threads, rounds = 8, 3
+    rng = np.random.default_rng(20261018)
+    # object sizes: small (one page shared by several), a few pages, ~1 MiB
+    sizes = [int(rng.integers(1, 5000)) for _ in range(threads)]
+    sizes[::3] = [int(rng.integers(40000, 70000)) for _ in sizes[::3]]
+    sizes[1::4] = [(1 << 20) + int(rng.integers(0, 99)) for _ in sizes[1::4]]
+    gap = 37
+    src = np.full(sum(sizes) + 64 * threads + 4096, GUARD, dtype=np.uint8)
+    src_off = _carve(src.size, sizes, gap, True)
+    for o, n in zip(src_off, sizes):
+        src[o:o + n] = rng.integers(0, 256, n, dtype=np.uint8)
+    fl = [oracle.fragment_len(K, n) for n in sizes]
+    # all threads' fragments in one array, and all decoded objects in another
+    frag_sizes = [f for f in fl for _ in range(K + M)]
+    frag = np.full(sum(frag_sizes) + 64 * len(frag_sizes) + 4096, GUARD, dtype=np.uint8)
+    frag_off = _carve(frag.size, frag_sizes, gap, True)
+    dec = np.full(sum(sizes) + 64 * threads + 4096, GUARD, dtype=np.uint8)
+    dec_off = _carve(dec.size, sizes, gap, True)
+    want = [oracle.encode(K, M, src[o:o + n].tobytes()) for o, n in zip(src_off, sizes)]
+    drivers = [_native.init(K, M, 11) for _ in range(threads // 2)]  # amd_rs_vand
+
+    def work(i):
+        h = drivers[i % len(drivers)]
+        n = sizes[i]
+        base = src.ctypes.data + src_off[i]
+        fptr = [frag.ctypes.data + frag_off[i * (K + M) + j] for j in range(K + M)]
+        for r in range(rounds):
+            for j in range(K + M):
+                o = frag_off[i * (K + M) + j]
+                frag[o:o + fl[i]] = 0
+            arr = (ctypes.c_void_p * (K + M))(*fptr)
+            rc = lib.ecamd_encode_into(h.desc, base, n, arr, fl[i])
+            assert rc == 0, f"encode rc {rc}"
+            for j in range(K + M):
+                o = frag_off[i * (K + M) + j]
+                assert frag[o:o + fl[i]].tobytes() == want[i][j], f"fragment {j} round {r}"
+            # decode from the last k + m - 4 fragments: 4 data fragments missing
+            avail = (ctypes.c_char_p * (K + M - 4))(
+                *[ctypes.cast(fptr[j], ctypes.c_char_p) for j in range(4, K + M)])
+            dec[dec_off[i]:dec_off[i] + n] = 0
+            rc = lib.ecamd_decode_into(h.desc, avail, K + M - 4, fl[i], 0,
+                                       dec.ctypes.data + dec_off[i], n)
+            assert rc == 0, f"decode rc {rc}"
+            assert dec[dec_off[i]:dec_off[i] + n].tobytes() == src[src_off[i]:src_off[i] + n].tobytes()
+
+    _run_threads(work, threads)
+    for arr, offs, lens in ((src, src_off, sizes), (frag, frag_off, frag_sizes), (dec, dec_off, sizes)):
+        mask = np.ones(arr.size, dtype=bool)
+        for o, n in zip(offs, lens):
+            mask[o:o + n] = False
+        assert np.all(arr[mask] == GUARD), "a call wrote outside its caller's buffer"
+    for h in drivers:
+        _native.destroy(h)
+    freed = [src.size, frag.size, dec.size]
+    del src, frag, dec
+    # pageable copies at the freed addresses' sizes and at round 4's faulting sizes
+    for n in freed + [1_048_576 + 99, 1_150_000, 1_258_752, 1_500_000]:
+        a = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8)
+        t = torch.from_numpy(a).to(gpu)
+        back = t.cpu().numpy()
+        assert np.array_equal(a, back)
+    torch.cuda.synchronize()
+
+
+def test_python_api_adjacent_bytes(oracle):
+    """ECDriver calls on many small bytes objects made back to back (adjacent
+    on the heap, sharing pages), 8 threads; then pageable torch copies."""
+    import torch
+    from pyeclib_amd import ECDriver
+    drv = ECDriver(k=K, m=M, ec_type="amd_rs_vand")
+    objs = [os.urandom(1000 + 7 * i) for i in range(64)]
+    wants = [oracle.encode(K, M, o) for o in objs]
+
+    def work(i):
+        for j in range(i, len(objs), 8):
+            frags = drv.encode(objs[j])
+            assert frags == wants[j]
+            assert drv.decode(frags[4:]) == objs[j]
+            assert drv.reconstruct(frags[1:], [0])[0] == frags[0]
+
+    _run_threads(work, 8)
+    drv.close()
+    for n in (1_150_000, 1_258_752):
+        a = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8)
+        assert np.array_equal(torch.from_numpy(a).to("cuda:0").cpu().numpy(), a)

@@ -18,6 +18,13 @@ for s in $STEPS; do
     (cd $R && timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
         --timeout-method thread > $O/pytest_gpu.log 2>&1)
     tail -3 $O/pytest_gpu.log ;;
+  tracetests)
+    # the whole GPU suite once under a kernel + memory-copy trace, so that a
+    # fault names the last dispatch or copy before it
+    (cd $R && timeout -k 10 900 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+        -d $O/trace -o run -- python3 -u -m pytest tests -m gpu -x -v --timeout 300 \
+        --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1)
+    tail -3 $O/pytest_gpu.log ;;
   newtests)
     (cd $R && timeout -k 10 600 python3 -u -m pytest tests/test_gpu_configs.py -m gpu -x -v --timeout 300 \
         --timeout-method thread > $O/pytest_gpu_new.log 2>&1)
