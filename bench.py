@@ -105,7 +105,7 @@ def parse(argv=None):
                     help="launches of the full-stripe encode (k data + m parity fragments, "
                          "headers included: liberasurecode_encode's output) timed after the "
                          "headline steps; 0 = skip")
-    ap.add_argument("--swift-procs", default="1,4,15",
+    ap.add_argument("--swift-procs", default="1,4,8",
                     help="process counts of the Swift call-shape leg (tools/swift_calls.py: "
                          "P processes calling ECDriver.encode / decode per segment); '' = skip")
     ap.add_argument("--swift-seconds", type=float, default=1.0)
@@ -936,7 +936,8 @@ def main():
         rows = swift_calls.sweep(procs, (1 << 20, 4 << 20), args.swift_seconds)
         result["swift_calls"] = {
             f"{r['op']}_{r['size'] >> 20}MiB_P{r['procs']}":
-                {"GiBps": r["GiBps"], "us_per_call": r["us_per_call_median"]} for r in rows}
+                ({"error": r["error"]} if "error" in r else
+                 {"GiBps": r["GiBps"], "us_per_call": r["us_per_call_median"]}) for r in rows}
         result["swift_calls_verified"] = all(r["verified"] for r in rows)
         result["swift_calls_note"] = (
             "P worker processes on this GPU, each its own ECDriver(10, 4, liberasurecode_rs_vand) "

@@ -55,6 +55,8 @@ def lib() -> ctypes.CDLL:
         L.orc_invert.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_int]
         L.orc_crc32.argtypes = [u8p, ctypes.c_uint64]
         L.orc_crc32.restype = ctypes.c_uint32
+        L.orc_crc32_legacy.argtypes = [u8p, ctypes.c_uint64]
+        L.orc_crc32_legacy.restype = ctypes.c_uint32
         L.orc_encode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
                                  u8p, ctypes.c_uint64, u8p]
         L.orc_decode.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
@@ -99,6 +101,22 @@ def invert(mat: list[list[int]]) -> list[list[int]]:
 
 def crc32(data: bytes) -> int:
     return lib().orc_crc32(data, len(data))
+
+
+def crc32_legacy(data: bytes) -> int:
+    return lib().orc_crc32_legacy(data, len(data))
+
+
+def legacy_headers(frag: bytes) -> bytes:
+    """An inline_crc32 fragment as liberasurecode writes it with
+    LIBERASURECODE_WRITE_LEGACY_CRC set: payload checksum and metadata
+    checksum from liberasurecode_crc32_alt (erasurecode_helpers.c
+    set_checksum / set_metadata_chksum)."""
+    size = int.from_bytes(frag[4:8], "little")
+    h = bytearray(frag[:HDR])
+    h[21:25] = crc32_legacy(frag[HDR:HDR + size]).to_bytes(4, "little")
+    h[67:71] = crc32_legacy(bytes(h[:59])).to_bytes(4, "little")
+    return bytes(h) + frag[HDR:]
 
 
 def encode(k: int, m: int, data: bytes, ct: int = CHKSUM_NONE,

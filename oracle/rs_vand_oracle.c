@@ -293,6 +293,27 @@ int orc_gf_div(int a, int b) { gf_init(); return gf_div(a, b); }
 int orc_invert(const int *in, int *out, int n) { gf_init(); return gj_invert(in, out, n); }
 uint32_t orc_crc32(const uint8_t *p, uint64_t n) { return (uint32_t)crc32(0L, p, (uInt)n); }
 
+/* liberasurecode_crc32_alt (upstream src/utils/chksum/crc32.c), the CRC
+ * written when LIBERASURECODE_WRITE_LEGACY_CRC is set: the reflected
+ * 0xEDB88320 table walk with a signed accumulator, so its right shift is
+ * arithmetic (launchpad bug 1666320). */
+uint32_t orc_crc32_legacy(const uint8_t *p, uint64_t n)
+{
+    static uint32_t t[256];
+    static int ready;
+    if (!ready) {
+        for (uint32_t i = 0; i < 256; i++) {
+            uint32_t c = i;
+            for (int b = 0; b < 8; b++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+            t[i] = c;
+        }
+        ready = 1;
+    }
+    int32_t c = (int32_t)0xFFFFFFFFu;
+    while (n--) c = (int32_t)(t[((uint32_t)c ^ *p++) & 0xFF] ^ (uint32_t)(c >> 8));
+    return (uint32_t)c ^ 0xFFFFFFFFu;
+}
+
 /* liberasurecode_encode: out receives k+m fragments of orc_fragment_len bytes */
 int orc_encode(int k, int m, int ct, uint32_t libec, const uint8_t *data, uint64_t len, uint8_t *out)
 {

@@ -88,14 +88,22 @@ Mat identity() {
   return m;
 }
 
-// Z_n: append n zero bytes to the (reflected) CRC register.
-Mat zeros(uint64_t n) {
+// One zero byte appended to the CRC register: zlib's step, or the legacy
+// one whose right shift is arithmetic (crc32_legacy).
+Mat zero_byte(bool legacy) {
   const Tables& tb = tables();
   Mat one;
   for (int b = 0; b < 32; ++b) {
     const uint32_t r = 1u << b;
-    one.col[b] = tb.t[0][r & 0xFF] ^ (r >> 8);
+    const uint32_t sh = legacy ? static_cast<uint32_t>(static_cast<int32_t>(r) >> 8) : r >> 8;
+    one.col[b] = tb.t[0][r & 0xFF] ^ sh;
   }
+  return one;
+}
+
+// Z_n: append n zero bytes to the (reflected) CRC register.
+Mat zeros(uint64_t n, bool legacy) {
+  Mat one = zero_byte(legacy);
   Mat acc = identity();
   while (n) {
     if (n & 1) acc = compose(one, acc);
@@ -105,30 +113,6 @@ Mat zeros(uint64_t n) {
   return acc;
 }
 
-bool inverse(const Mat& m, Mat& out) {
-  // rows[i] bit j = m[i][j]; augment with identity, Gauss-Jordan over GF(2)
-  uint64_t rows[32];
-  for (int i = 0; i < 32; ++i) {
-    uint32_t r = 0;
-    for (int j = 0; j < 32; ++j) r |= (m.col[j] >> i & 1u) << j;
-    rows[i] = r | (uint64_t(1) << (32 + i));
-  }
-  for (int c = 0; c < 32; ++c) {
-    int p = c;
-    while (p < 32 && !(rows[p] >> c & 1)) ++p;
-    if (p == 32) return false;
-    std::swap(rows[p], rows[c]);
-    for (int r = 0; r < 32; ++r)
-      if (r != c && (rows[r] >> c & 1)) rows[r] ^= rows[c];
-  }
-  for (int j = 0; j < 32; ++j) {
-    uint32_t col = 0;
-    for (int i = 0; i < 32; ++i) col |= static_cast<uint32_t>(rows[i] >> (32 + j) & 1) << i;
-    out.col[j] = col;
-  }
-  return true;
-}
-
 void nibble_tables(const Mat& m, uint32_t (*t)[16]) {
   for (int q = 0; q < 8; ++q)
     for (uint32_t v = 0; v < 16; ++v) t[q][v] = apply(m, v << (4 * q));
@@ -136,44 +120,49 @@ void nibble_tables(const Mat& m, uint32_t (*t)[16]) {
 
 }  // namespace
 
-void build_crc_tables(uint32_t bs, uint32_t steps, CrcTables* out) {
+void build_crc_lane_tables(bool legacy, CrcLaneTables* out) {
   const Tables& tb = tables();
   std::memset(out, 0, sizeof(*out));
-  // raw CRC of a 16-byte chunk with byte i = v << 4h and zeros elsewhere:
-  // T0[byte] after byte i, then 15 - i zero bytes
-  Mat tail[16];
-  for (int i = 0; i < 16; ++i) tail[i] = zeros(15 - i);
-  for (int p = 0; p < 32; ++p) {
-    const int i = p / 2, h = p % 2;
-    for (uint32_t v = 0; v < 16; ++v) out->raw16[p][v] = apply(tail[i], tb.t[0][(v << (4 * h)) & 0xFF]);
+  // raw CRC of a 16-byte piece with byte i = v << 4h and zeros elsewhere: the
+  // byte's step from a zero register (T0[byte] in both variants), then 15 - i
+  // zero bytes
+  for (int i = 0; i < 16; ++i) {
+    const Mat tail = zeros(15 - i, legacy);
+    for (int h = 0; h < 2; ++h)
+      for (uint32_t v = 0; v < 16; ++v) out->raw16[2 * i + h][v] = apply(tail, tb.t[0][(v << (4 * h)) & 0xFF]);
   }
-  nibble_tables(zeros(4096), out->z4096);
-  for (int l = 0; l < 8; ++l) nibble_tables(zeros(uint64_t(16) << l), out->level[l]);
-  nibble_tables(zeros(8192), out->z8192);
-  nibble_tables(zeros(12288), out->z12288);
-  nibble_tables(zeros(16384), out->z16384);
-  Mat inv;
-  const uint64_t pad = uint64_t(steps) * 4096 - bs;
-  if (!inverse(zeros(pad), inv)) inv = identity();  // Z_n is always invertible (x is a unit mod P)
-  nibble_tables(inv, out->unshift);
-  for (int i = 0; i < 256; ++i) out->t0[i] = tb.t[0][i];
-  out->init_term = apply(zeros(bs), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+  for (int l = 0; l < 64; ++l) {
+    uint32_t t[8][16];
+    nibble_tables(zeros(uint64_t(16) * (63 - l), legacy), t);
+    for (int q = 0; q < 8; ++q)
+      for (int v = 0; v < 16; ++v) out->lane[q][v][l] = t[q][v];
+  }
 }
 
-void build_crc_finish_tables(uint32_t bs, uint32_t tiles_total, CrcFinishTables* out) {
+void build_crc_finish_tables(uint32_t bs, bool legacy, CrcFinishTables* out) {
   const Tables& tb = tables();
   std::memset(out, 0, sizeof(*out));
-  Mat z = zeros(4096);
+  Mat z = zeros(1024, legacy);
   for (int i = 0; i < kCrcPowBits; ++i) {
     nibble_tables(z, out->pow[i]);
     z = compose(z, z);
   }
-  Mat inv;
-  const uint64_t pad = uint64_t(tiles_total) * 4096 - bs;
-  if (!inverse(zeros(pad), inv)) inv = identity();  // Z_n is always invertible
-  nibble_tables(inv, out->unshift);
-  for (int i = 0; i < 256; ++i) out->t0[i] = tb.t[0][i];
-  out->init_term = apply(zeros(bs), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+  nibble_tables(zeros(bs % 1024, legacy), out->zr);
+  // metadata checksum change: the raw CRC of chksum[0]'s 4 bytes (header
+  // bytes 21..24), followed by the 34 bytes to the end of the 59-byte block
+  Mat meta;
+  for (int b = 0; b < 32; ++b) {
+    const uint32_t c = 1u << b;
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t x = (r ^ (c >> (8 * i))) & 0xFF;
+      const uint32_t sh = legacy ? static_cast<uint32_t>(static_cast<int32_t>(r) >> 8) : r >> 8;
+      r = tb.t[0][x] ^ sh;
+    }
+    meta.col[b] = apply(zeros(59 - 25, legacy), r);
+  }
+  nibble_tables(meta, out->meta);
+  out->init_term = apply(zeros(bs, legacy), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
 }
 
 }  // namespace ecamd

@@ -21,43 +21,44 @@ uint32_t crc32_legacy(uint32_t crc, const void* buf, size_t len);
 
 namespace ecamd {
 
-// Tables for the GPU payload CRC (ec_crc.hip).  A zlib CRC-32 register is
-// GF(2)-linear in the message: with raw(M) the register after M from a zero
-// start, crc32(0, M) = raw(M) ^ Z_n(0xFFFFFFFF) ^ 0xFFFFFFFF, where Z_n
-// appends n zero bytes, and raw(A || B) = Z_|B|(raw(A)) ^ raw(B).  Every
-// linear map is stored as nibble tables [q 0..7][v 0..15] (u32) so that
-// map(r) = XOR_q T[q][nibble_q(r)] -- eight conflict-free LDS lookups.
-struct CrcTables {
-  uint32_t raw16[32][16];     // raw CRC of a 16-byte chunk, per nibble position
-  uint32_t z4096[8][16];      // Z_4096
-  uint32_t level[8][8][16];   // Z_{16 * 2^l}, l = 0..7 (lane tree)
-  uint32_t z8192[8][16];      // Z_8192, Z_12288, Z_16384: the loader / consumer encode's
-  uint32_t z12288[8][16];     // wave tree and Horner steps (12 / 16 KiB items)
-  uint32_t z16384[8][16];
-  uint32_t unshift[8][16];    // Z_pad^-1: drops the zero padding past the payload
-  uint32_t t0[256];           // bytewise table (header metadata CRC)
-  uint32_t init_term;         // Z_bs(0xFFFFFFFF) ^ 0xFFFFFFFF
-  uint32_t pad[3];
+// Tables for the GPU payload CRC.  A CRC-32 register is GF(2)-linear in the
+// message: with raw(M) the register after M from a zero start,
+// crc32(0, M) = raw(M) ^ Z_n(0xFFFFFFFF) ^ 0xFFFFFFFF, where Z_n appends n
+// zero bytes, and raw(A || B) = Z_|B|(raw(A)) ^ raw(B).  That holds for the
+// legacy variant too (its arithmetic shift is linear as well), with its own
+// Z.  Every linear map is stored as nibble tables -- map(r) = XOR_q
+// T[q][nibble_q(r)] -- eight LDS lookups.
+//
+// The kernels take the raw CRC of each 1 KiB chunk a wave holds (lane l
+// holding bytes [16 l, 16 l + 16)): raw(chunk) = XOR_l Z_{16 (63 - l)}(
+// raw16(piece_l)), i.e. per lane the 32 lookups of raw16 and the 8 of its
+// own lane map, then an XOR across the wave (no shifts between lanes).
+struct CrcLaneTables {
+  uint32_t raw16[32][16];     // raw CRC of a 16-byte piece, per nibble position
+  uint32_t lane[8][16][64];   // Z_{16 (63 - l)}: [q][v][lane], lane-minor, so the
+                              // 64 lanes of a lookup hit 64 different banks
 };
-static_assert(sizeof(CrcTables) % 16 == 0, "CrcTables is copied to LDS in 16-B pieces");
+static_assert(sizeof(CrcLaneTables) % 16 == 0, "copied to LDS in 16-B pieces");
 
-// Tables for payloads of `bs` bytes processed in `steps` rounds of 4 KiB.
-void build_crc_tables(uint32_t bs, uint32_t steps, CrcTables* out);
-
-// The encode kernel's fused parity CRC (ec_kernels_impl.hpp) leaves one raw
-// CRC per run of 4 KiB tiles; the finishing pass (ec_crc.hip) shifts each to
-// the end of the zero-padded payload, XORs them, removes the padding and
-// folds in the init / final XORs.
-constexpr int kCrcPowBits = 20;  // tiles_total < 2^20 (payloads < 4 GiB)
+// The finishing pass (ec_crc.hip) shifts every chunk's raw CRC to the end
+// of the bs-byte payload -- chunk c ends at 1024 (c + 1), so by Z_r after
+// Z_{1024 a}, r = bs mod 1024 -- XORs them with the payload tail's (read
+// back, end-aligned: no zero padding to remove), and folds in the init /
+// final XORs.  The header's metadata checksum was computed on the host with
+// chksum[0] = 0; the checksum of the same 59 bytes with chksum[0] = c
+// differs from it by meta(c), a linear map of c (the init and final terms
+// cancel between two messages of one length).
+constexpr int kCrcPowBits = 22;  // bs / 1024 < 2^22 (payloads < 4 GiB)
 struct CrcFinishTables {
-  uint32_t pow[kCrcPowBits][8][16];  // Z_{4096 * 2^i}
-  uint32_t unshift[8][16];           // Z_pad^-1, pad = tiles_total * 4096 - bs
-  uint32_t t0[256];                  // bytewise table (header metadata CRC)
+  uint32_t pow[kCrcPowBits][8][16];  // Z_{1024 * 2^i}
+  uint32_t zr[8][16];                // Z_{bs mod 1024}
+  uint32_t meta[8][16];              // c (header bytes 21..24) -> metadata checksum change
   uint32_t init_term;                // Z_bs(0xFFFFFFFF) ^ 0xFFFFFFFF
   uint32_t pad[3];
 };
 static_assert(sizeof(CrcFinishTables) % 16 == 0, "copied to LDS in 16-B pieces");
 
-void build_crc_finish_tables(uint32_t bs, uint32_t tiles_total, CrcFinishTables* out);
+void build_crc_lane_tables(bool legacy, CrcLaneTables* out);
+void build_crc_finish_tables(uint32_t bs, bool legacy, CrcFinishTables* out);
 
 }  // namespace ecamd

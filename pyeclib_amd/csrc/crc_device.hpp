@@ -1,13 +1,17 @@
 // Device side of the GPU payload CRC-32: GF(2)-linear maps applied by
 // nibble-table lookups in LDS (tables built by crc32.cpp, layout
-// [q 0..7][v 0..15] u32 per 32-bit map; [p 0..31][v 0..15] for raw16).
-// Shared by the CRC pass (ec_crc.hip) and the fused parity CRC of the encode
-// kernel (ec_kernels_impl.hpp).
+// [q 0..7][v 0..15] u32 per 32-bit map; [p 0..31][v 0..15] for raw16;
+// CrcLaneTables::lane [q][v][lane]).  Shared by the region kernels, which
+// take each 1 KiB chunk's raw CRC as they write it (ec_kernels_impl.hpp), and
+// the finishing pass (ec_crc.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdint>
+
+#include "crc32.hpp"
 
 namespace ecamd {
 namespace crcdev {
@@ -70,32 +74,42 @@ __device__ __forceinline__ uint32_t raw_dword(uint32_t w, int d, uint32_t tab) {
   return a;
 }
 
-// zlib crc32 of the 59-byte metadata block of a header held as 16 dwords
-// (bytewise table t0 at LDS byte `t0`).
-__device__ __forceinline__ uint32_t meta_crc(const uint32_t (&h)[16], uint32_t t0) {
-  uint32_t m = 0xFFFFFFFFu;
-  for (int b = 0; b < 59; ++b) m = lds32(t0 + 4 * ((m ^ byte_of(h[b >> 2], b & 3)) & 0xFF)) ^ (m >> 8);
-  return m ^ 0xFFFFFFFFu;
+// Z_{16 (63 - l)}(r) for this lane: the lane-minor tables at LDS byte
+// `tab`, lane4 = 4 * lane.
+__device__ __forceinline__ uint32_t lane_map(uint32_t r, uint32_t tab, uint32_t lane4) {
+  uint32_t a = 0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) a ^= lds32(tab + 4096u * q + (((r >> (4 * q)) & 15u) << 8) + lane4);
+  asm volatile("" : "+v"(a));
+  return a;
 }
 
-// Patch chksum[0] (header bytes 21..24) with `crc` and then the metadata
-// checksum (bytes 67..70) of the fragment header at `frag`.
-__device__ __forceinline__ void patch_header(uint8_t* frag, uint32_t crc, uint32_t t0) {
-  uint32_t h[16];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint4 v = reinterpret_cast<const uint4*>(frag)[q];
-    h[4 * q] = v.x;
-    h[4 * q + 1] = v.y;
-    h[4 * q + 2] = v.z;
-    h[4 * q + 3] = v.w;
+// XOR of a over the 64 lanes of the wave (wave-uniform): DPP within each row
+// of 16 lanes, then the four rows' values read out.
+__device__ __forceinline__ uint32_t wave_xor(uint32_t a) {
+  a ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(a), 0xB1, 0xF, 0xF, false));
+  a ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(a), 0x4E, 0xF, 0xF, false));
+  a ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(a), 0x141, 0xF, 0xF, false));
+  a ^= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(a), 0x140, 0xF, 0xF, false));
+  return __builtin_amdgcn_readlane(a, 0) ^ __builtin_amdgcn_readlane(a, 16) ^
+         __builtin_amdgcn_readlane(a, 32) ^ __builtin_amdgcn_readlane(a, 48);
+}
+
+// Raw CRC of the wave's 1 KiB chunk, lane l holding bytes [16 l, 16 l + 16)
+// in v (CrcLaneTables at LDS byte `tab`): wave-uniform.
+__device__ __forceinline__ uint32_t chunk_crc(const uint4& v, uint32_t tab, uint32_t lane4) {
+  return wave_xor(lane_map(raw16(v, tab), tab + offsetof(CrcLaneTables, lane), lane4));
+}
+
+// Set chksum[0] (header bytes 21..24) of the fragment header at `frag` to
+// `crc` (it was 0) and update the metadata checksum (bytes 67..70) by the
+// change that makes (CrcFinishTables::meta at LDS byte `meta`).
+__device__ __forceinline__ void patch_header(uint8_t* frag, uint32_t crc, uint32_t meta) {
+  const uint32_t d = zmap(crc, meta);
+  for (int b = 0; b < 4; ++b) {
+    frag[21 + b] = static_cast<uint8_t>(crc >> (8 * b));
+    frag[67 + b] = static_cast<uint8_t>(frag[67 + b] ^ (d >> (8 * b)));
   }
-  // chksum occupies bytes 21..24: bytes 21..23 in h[5] (bits 8..31), 24 in h[6]
-  h[5] = (h[5] & 0x000000FFu) | (crc << 8);
-  h[6] = (h[6] & 0xFFFFFF00u) | (crc >> 24);
-  const uint32_t m = meta_crc(h, t0);
-  for (int b = 21; b < 25; ++b) frag[b] = static_cast<uint8_t>(crc >> (8 * (b - 21)));
-  for (int b = 67; b < 71; ++b) frag[b] = static_cast<uint8_t>(m >> (8 * (b - 67)));
 }
 
 }  // namespace crcdev

@@ -12,15 +12,15 @@
 namespace ecamd {
 
 // GF(2^16) encode: <= 2 rows per pass need only the low dword of each table
-// entry (Gf16<1>); 5..8 rows run in one eight-row pass (Gf16x8, its rows
-// past p.nrows dropped).
+// entry (Gf16<1>); 5..8 rows run in one eight-row pass (Gf16x8).  A pass is
+// built for 2, 4 or 8 rows; the rows past p.nrows are dropped
+// (ec_kernels_impl.hpp parity_row), so 1, 3, 5..7 rows need no kernels of
+// their own.
 #define ECAMD_ENC16(K)                                                      \
   hipError_t launch_enc16_##K(const EncodeParams& p, hipStream_t s) {       \
     switch (p.nrows) {                                                      \
-      case 1: return launch_encode_k<Gf16<1>, K, 1>(p, s);                  \
-      case 2: return launch_encode_k<Gf16<1>, K, 2>(p, s);                  \
-      case 3: return launch_encode_k<Gf16<2>, K, 3>(p, s);                  \
-      case 4: return launch_encode_k<Gf16<2>, K, 4>(p, s);                  \
+      case 1: case 2: return launch_encode_k<Gf16<1>, K, 2>(p, s);          \
+      case 3: case 4: return launch_encode_k<Gf16<2>, K, 4>(p, s);          \
       case 5: case 6: case 7: case 8:                                       \
         return launch_encode_k<Gf16x8, K, 8>(p, s);                         \
       default: return hipErrorInvalidValue;                                 \
@@ -42,9 +42,12 @@ namespace ecamd {
     }                                                                           \
   }
 
+// GF(2^8): one table entry carries four rows whatever the pass holds, so
+// every pass runs the four-row kernel (rows past p.nrows dropped).
 #define ECAMD_ENC8(K)                                                 \
   hipError_t launch_enc8_##K(const EncodeParams& p, hipStream_t s) {  \
-    return launch_encode_rows<Gf8, K>(p, s);                          \
+    if (p.nrows < 1 || p.nrows > 4) return hipErrorInvalidValue;      \
+    return launch_encode_k<Gf8, K, 4>(p, s);                          \
   }
 
 #define ECAMD_DEC8(K)                                                           \

@@ -77,19 +77,16 @@ struct EncodeParams {
                                // items; 0 = every block runs its share of them first
   uint32_t no_edge_blocks;     // caller: 1 = never run the edge items in blocks of their own
                                // (the round-2 launch form; instance knob ECAMD_EDGE_BLOCKS=0)
-  // inline_crc32 fused into the encode (null: no parity CRC in this launch):
-  // CrcTables (its raw16 / z4096 / level maps), CrcFinishTables for
-  // (bs, ceil(bs / 4096)), and n_obj * ceil(bs / 4096) * m u32 of run
-  // partials (ec_crc.hpp CrcFinishParams)
-  const void* crc_tables;
-  const void* crc_finish_tables;
+  // inline_crc32 (crc_lanes null: none).  The launch takes the raw CRC of
+  // every 1 KiB chunk of the interior it writes -- parity rows into
+  // crc_part[(o * chunks + c) * m + row], with the full stripe the data
+  // fragments into crc_part_data[(o * chunks + c) * k + j], chunks = the
+  // interior's 1 KiB chunks per payload (<= bs / 1024) -- and the launcher
+  // then runs the finishing pass (ec_crc.hpp) over those fragments.
+  const void* crc_lanes;         // CrcLaneTables (crc32.hpp), device memory
+  const void* crc_finish_tables; // CrcFinishTables for bs, device memory
   uint32_t* crc_part;
-  // full-stripe encode with the CRC: room for the data fragments' run
-  // partials (n_obj * ceil(bs / 4096) * k u32).  The launcher fuses their CRC
-  // when it takes the loader / consumer CRC kernel and then sets the HOST
-  // flag *crc_data_fused = 1; otherwise the caller runs the CRC pass.
   uint32_t* crc_part_data;
-  uint32_t* crc_data_fused;
 };
 
 // Loader / consumer kernels (ec_kernels_impl.hpp encode_dma_kernel ...):
@@ -145,6 +142,12 @@ struct DecodeParams {
   uint32_t edge_blocks;        // set by the launcher (see EncodeParams)
   uint32_t no_edge_blocks;     // caller (see EncodeParams)
   uint32_t tile_ch;            // set by the launcher: 4 KiB tiles per interior item
+  // reconstruct with inline_crc32 (crc_lanes null: none): the raw CRC of every
+  // 1 KiB interior chunk of fragment o into crc_part[o * chunks + c], then the
+  // finishing pass (see EncodeParams)
+  const void* crc_lanes;
+  const void* crc_finish_tables;
+  uint32_t* crc_part;
 };
 
 // Dispatch on (p.w, p.k) to the per-k instantiations (ec_dispatch.cpp).

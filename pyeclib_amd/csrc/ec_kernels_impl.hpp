@@ -707,16 +707,15 @@ __device__ __forceinline__ void enc_item_pos(const EncodeParams& p, uint32_t w, 
   x = (w - o * p.tiles) * (kTile * CH) + wave_in_block() * (kChunkBytes * CH);
 }
 
-// Parity row q's store descriptor.  An eight-row pass (Gf16x8, m = 5..7)
-// computes rows past m from zero coefficients: their stores go through a
-// zero-record descriptor and are dropped, so every item still issues the
-// same instructions.
+// Parity row q's store descriptor.  A pass computes NR rows (2, 4 or 8: the
+// kernels are instantiated for those only) and the pass may hold fewer
+// (p.nrows: m = 1, 3, 5..7); the rows past p.nrows come from zero
+// coefficients and their stores go through a zero-record descriptor and are
+// dropped, so every item still issues the same instructions.
 template <int NR>
 __device__ __forceinline__ Rsrc parity_row(const EncodeParams& p, uint32_t o, int q, Rsrc par) {
-  if constexpr (NR > kRowsPerPass)
-    return rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride,
-                static_cast<uint32_t>(q) < p.nrows ? -1 : 0);
-  return par;
+  if (q == 0 || static_cast<uint32_t>(q) < p.nrows) return par;  // every pass has a first row
+  return rsrc(p.parity, 0);
 }
 
 // Inputs an edge item holds in registers at once (edge items run inside the
@@ -772,6 +771,35 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
            zero_tail(F::row(s, q), rem));
 }
 
+// ---------------- inline CRC-32 of the chunks a launch writes ----------------
+//
+// inline_crc32 (liberasurecode's set_checksum, upstream erasurecode_helpers.c;
+// pyeclib core.py:59-63 -> pyeclib_c.c:248): every wave takes the raw CRC of
+// each 1 KiB fragment chunk it writes while the chunk is in its registers
+// (crc_device.hpp chunk_crc: per lane raw16 and its lane map, 40 nibble
+// lookups per 16 B, then an XOR across the wave) and one lane stores it; the
+// finishing pass (ec_crc.hip) shifts the chunks' CRCs into place and reads
+// back only the edge items' bytes.  The partials are independent of the
+// order items are dealt in, so the CRC kernels walk the items exactly as the
+// plain ones do.  (Rounds 2-4 kept a Horner accumulator per thread instead,
+// which needs each block to walk a contiguous item range, and joined the
+// threads at every run end behind block barriers: 1.21-1.26x the plain
+// encode, 10 % of it the order; profiles/r04n_ab_contig.txt.)  The lane
+// tables (CrcLaneTables, 34 KiB) sit in LDS after the GF tables.
+constexpr uint32_t kCrcLaneBytes = sizeof(CrcLaneTables);
+template <class F, int K>
+__host__ __device__ constexpr uint32_t crc_lds_base() {
+  return (K * F::kTableBytes + 255u) & ~255u;
+}
+// 1 KiB chunks of every payload covered by a launch's interior items.
+__host__ __device__ constexpr uint32_t crc_chunks(uint32_t tiles, uint32_t tile_ch) {
+  return tiles * tile_ch * (kTile / kChunkBytes);
+}
+// A wave-uniform raw CRC stored by one lane (a vector store).
+__device__ __forceinline__ void crc_store(uint32_t* dst, uint32_t v) {
+  if (lane_id() == 0) *dst = v;
+}
+
 // Interior encode: object slices streamed in (default cache policy --
 // neighbouring slices share 128-B lines, which L2 then serves twice), parity
 // chunks stored nontemporal and line-aligned.  DATA (full-stripe encode,
@@ -780,7 +808,8 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
 // its data fragment's line-aligned payload before the registers are refilled
 // -- one pass over the object instead of a separate copy.  NOCOMP:
 // memory-only probe (inputs XORed, no lookups; wrong parity) for the
-// benchmark shape.
+// benchmark shape.  CRC: inline_crc32 partials of the parity chunks (and of
+// the data chunks, DATA), CH = 1.
 //
 // CH (A/B, k = 10): an item spans CH * 4 KiB of payload positions and each
 // wave takes CH KiB contiguous of every slice; the stream runs chunk-major
@@ -802,9 +831,12 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
 // without -- the deeper stream costs more at the HBM than the drain did --
 // so the encode keeps HEAD = false; decode (decode_interior) keeps its own.
 template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false, int CH = 1,
-          bool NTL = false, int NBX = 0, bool HEAD = false>
+          bool NTL = false, int NBX = 0, bool HEAD = false, bool CRC = false>
 __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
   constexpr int NB = NBX ? NBX : stream_bufs<K>();  // NBX: A/B (divides K)
+  static_assert(!CRC || CH == 1, "CRC partials per 1 KiB chunk");
+  const uint32_t chunks = crc_chunks(p.tiles, p.tile_ch);
+  const uint32_t lane4 = lane_id() * 4;
   const ItemRange r = item_range(p.n_obj * p.tiles, p.xcd_split, interior_block(p.edge_blocks));
   uint32_t w = r.begin;
   if (w >= r.end) return;
@@ -853,8 +885,12 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
         } else {
           F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[i % NB], s);
         }
-        if constexpr (DATA)
+        if constexpr (DATA) {
           buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x + kChunkBytes * c, buf[i % NB]);
+          if constexpr (CRC)
+            crc_store(p.crc_part_data + (static_cast<uint64_t>(o) * chunks + x / kChunkBytes) * K + j,
+                      crcdev::chunk_crc(buf[i % NB], crc_lds_base<F, K>(), lane4));
+        }
       }
       const int in = i + NB;  // slot refilled into this buffer
       if (in < SL) {
@@ -868,6 +904,13 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
 #pragma unroll
         for (int q = 0; q < NR; ++q)
           buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, F::row(s, q));
+        if constexpr (CRC) {
+          uint32_t* part = p.crc_part + (static_cast<uint64_t>(o) * chunks + x / kChunkBytes) * p.m + p.row0;
+#pragma unroll
+          for (int q = 0; q < NR; ++q)
+            if (static_cast<uint32_t>(q) < p.nrows)
+              crc_store(part + q, crcdev::chunk_crc(F::row(s, q), crc_lds_base<F, K>(), lane4));
+        }
         if (c + 1 < CH) F::zero(s);
       }
     }
@@ -903,9 +946,10 @@ __device__ __forceinline__ void encode_edges(const EncodeParams& p, uint32_t fir
 // Register budget (waves per SIMD) of an encode instantiation.  GF(2^8)
 // with k >= 18 (six inputs in flight, 4-byte table entries) spilled 12 B per
 // lane at 64 VGPRs and gets 72.
-template <class F, int K, bool DATA, int NBX>
+template <class F, int K, bool DATA, int NBX, bool CRC = false>
 __host__ __device__ constexpr int encode_occ() {
   if (F::kRows > kRowsPerPass) return 4;  // eight-row accumulators: 32 VGPRs
+  if (CRC) return DATA ? kEncodeCrcDataOcc : (stream_bufs<K>() >= 6 ? 6 : kEncodeCrcOcc);
   if (DATA) return kEncodeDataOcc;
   if (NBX > 6) return 4;
   if (F::kW == 8 && K >= 18) return 7;
@@ -913,11 +957,13 @@ __host__ __device__ constexpr int encode_occ() {
 }
 
 template <class F, int K, int NR, bool NOCOMP = false, bool DATA = false, int CH = 1,
-          bool NTL = false, int NBX = 0, bool HEAD = false>
+          bool NTL = false, int NBX = 0, bool HEAD = false, bool CRC = false>
 __global__ void __launch_bounds__(kThreadsPerBlock)
-    __attribute__((amdgpu_waves_per_eu(encode_occ<F, K, DATA, NBX>(), 8)))
+    __attribute__((amdgpu_waves_per_eu(encode_occ<F, K, DATA, NBX, CRC>(), 8)))
     encode_kernel(EncodeParams p) {
   load_tables(p.tables, K * F::kTableBytes, 0);
+  if constexpr (CRC)
+    load_tables(static_cast<const uint32_t*>(p.crc_lanes), kCrcLaneBytes, crc_lds_base<F, K>());
   __syncthreads();
   if (p.fused_edges) {
     if (p.edge_blocks == 0) {
@@ -927,7 +973,7 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
       return;
     }
   }
-  encode_interior<F, K, NR, NOCOMP, DATA, CH, NTL, NBX, HEAD>(p);
+  encode_interior<F, K, NR, NOCOMP, DATA, CH, NTL, NBX, HEAD, CRC>(p);
 }
 
 // Headers and edge items of an encode in a launch of their own (the
@@ -958,6 +1004,10 @@ __global__ void __launch_bounds__(kThreadsPerBlock) encode_edge_kernel(EncodePar
 // t - 1.  The DMAs are inline asm (hipcc does not see them, so it neither
 // drains them before LDS reads nor counts them); the waits are explicit.
 // Edge items and headers run in blocks of their own, 256 threads of them.
+// inline_crc32 (p.crc_lanes set, a runtime switch: the kernel's register
+// budget has room): the lane tables follow the GF tables in LDS, the ring
+// after them, and every consumer wave stores its parity chunks' (and, with
+// DATA, its data chunks') raw CRCs.
 constexpr uint32_t kDmaSlot = 8192;  // bytes of a ring slot per KiB of SW (8 waves x 1 KiB)
 constexpr uint32_t kDmaThreads = 512;
 
@@ -1006,8 +1056,8 @@ __host__ __device__ constexpr uint32_t dma_ring_base() {
 // SW: KiB of each slot a consumer wave takes (slot = 8 * SW KiB, item = one
 // slot's positions across the k inputs); L: loader waves.
 template <class F, int K, int R, int SW, int W = 8>
-__host__ __device__ constexpr uint32_t dma_lds_bytes() {
-  return dma_ring_base<F, K>() + R * 1024 * W * SW;
+__host__ __device__ constexpr uint32_t dma_lds_bytes(bool crc = false) {
+  return dma_ring_base<F, K>() + (crc ? kCrcLaneBytes : 0u) + R * 1024 * W * SW;
 }
 
 // W: waves per block (8 = 2 per SIMD, 16 = 4 per SIMD).  DATA: the consumers
@@ -1034,8 +1084,11 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
     encode_edges<F, K, NR, DATA>(p, blockIdx.x, p.edge_blocks);
     return;
   }
+  const bool crc = p.crc_lanes != nullptr;
   for (uint32_t i = threadIdx.x; i < K * F::kTableBytes / 16; i += W * 64)
     lds_v4(0)[i] = reinterpret_cast<const v4u*>(p.tables)[i];
+  if (crc)
+    load_tables(static_cast<const uint32_t*>(p.crc_lanes), kCrcLaneBytes, dma_ring_base<F, K>(), W * 64);
   __syncthreads();
   ItemRange rg = item_range(p.n_obj * p.tiles, p.xcd_split, interior_block(p.edge_blocks));
   if constexpr (CONTIG) {
@@ -1065,8 +1118,9 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
     n_items = to_sgpr((rg.end - rg.begin + rg.step - 1) / rg.step);
   }
   const bool loader = wave < static_cast<uint32_t>(L);
-  const uint32_t lane16 = lane_id() * 16;
-  constexpr uint32_t kRing = dma_ring_base<F, K>();
+  const uint32_t lane16 = lane_id() * 16, lane4 = lane_id() * 4;
+  const uint32_t kRing = to_sgpr(dma_ring_base<F, K>() + (crc ? kCrcLaneBytes : 0u));
+  const uint32_t chunks = crc_chunks(p.tiles, p.tile_ch);
   // item i of this block: object and first payload position
   auto item_at = [&](uint32_t i, uint32_t& o, uint32_t& x0) {
     if constexpr (COMB > 0) {
@@ -1126,8 +1180,12 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
         } else {
           F::template mac<true>(F::kb(0), j * F::kTableBytes, x, s[c]);
         }
-        if constexpr (DATA)
+        if constexpr (DATA) {
           buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x0 + (wave * SW + c) * 1024, x);
+          if (crc)
+            crc_store(p.crc_part_data + (static_cast<uint64_t>(o) * chunks + x0 / 1024 + wave * SW + c) * K + j,
+                      crcdev::chunk_crc(x, dma_ring_base<F, K>(), lane4));
+        }
       }
       ring = ring + 1 == R ? 0 : ring + 1;
     }
@@ -1138,400 +1196,14 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
 #pragma unroll
       for (int q = 0; q < NR; ++q)
         buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, F::row(s[c], q));
+      if (crc) {
+        uint32_t* part = p.crc_part + (static_cast<uint64_t>(o) * chunks + x0 / 1024 + wave * SW + c) * p.m + p.row0;
+#pragma unroll
+        for (int q = 0; q < NR; ++q)
+          if (static_cast<uint32_t>(q) < p.nrows)
+            crc_store(part + q, crcdev::chunk_crc(F::row(s[c], q), dma_ring_base<F, K>(), lane4));
+      }
       F::zero(s[c]);
-    }
-  }
-  if (loader) wait_vm<0>();  // no DMA may land in LDS after the block ends
-}
-
-// ---------------- encode with the parity CRC fused (inline_crc32) ----------------
-//
-// liberasurecode's set_checksum (upstream erasurecode_helpers.c; pyeclib
-// core.py:59-63 -> pyeclib_c.c:248) writes zlib crc32(0, payload, bs) into
-// every fragment header.  A separate CRC pass re-reads every parity payload
-// and is lookup-bound (measured round 2: +136 us on the 310-us encode at
-// 256 x 4 MiB, profiles/r02p); here the encode kernel takes the raw CRC of
-// the parity chunks it has just computed, in registers.
-//
-// The raw CRC is GF(2)-linear: raw(A || B) = Z_|B|(raw(A)) ^ raw(B).  Each
-// block walks a CONTIGUOUS range of interior items (not grid-stride), so a
-// thread's consecutive pieces of one parity payload are 4 KiB apart and it
-// keeps their raw CRC in Horner form acc = Z_4096(acc) ^ raw16(piece) (40
-// nibble lookups per 16 B and row).  When the range leaves an object (or
-// ends), the block joins its 256 threads with the lane tree of the CRC pass
-// and stores one raw CRC per row for that run.  crc_finish_kernel (one block
-// per parity fragment) takes the edge tiles' raw CRC from the payload just
-// written, shifts every run to the end of the payload and finishes the
-// header.  Data fragments, when materialised, keep the CRC pass.
-
-constexpr uint32_t kCrcLdsBytes = offsetof(CrcTables, unshift);  // raw16, z4096, level[8]
-constexpr uint32_t kCrcZ4096 = offsetof(CrcTables, z4096);
-constexpr uint32_t kCrcLevel = offsetof(CrcTables, level);
-template <class F, int K>
-__host__ __device__ constexpr uint32_t crc_lds_base() {
-  return (K * F::kTableBytes + 255u) & ~255u;
-}
-template <class F, int K>
-__host__ __device__ constexpr uint32_t crc_lds_bytes() {
-  return crc_lds_base<F, K>() + kCrcLdsBytes + 4 * kWavesPerBlock * 4;  // + run partials
-}
-
-// Join the block's 256 per-thread raw CRCs of NR rows (thread t's pieces at
-// 16 t within each tile) and store row q's at dst[q]; zeroes acc.  Block-uniform.
-template <int NR>
-__device__ __forceinline__ void crc_block_flush(uint32_t (&acc)[NR], uint32_t base, uint32_t* dst) {
-  const uint32_t lane = lane_id(), wave = wave_in_block();
-  const uint32_t lev = base + kCrcLevel, red = base + kCrcLdsBytes;
-#pragma unroll
-  for (int q = 0; q < NR; ++q) {
-    uint32_t a = acc[q];
-#pragma unroll
-    for (int l = 0; l < 6; ++l) {
-      const uint32_t other = __shfl_down(a, 1u << l, 64);
-      a = crcdev::zmap(a, lev + 512u * l) ^ other;
-    }
-    if (lane == 0)
-      *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
-          static_cast<uintptr_t>(red + 4 * (wave * NR + q))) = a;
-    acc[q] = 0;
-  }
-  __syncthreads();
-  if (threadIdx.x < static_cast<uint32_t>(NR)) {
-    const uint32_t q = threadIdx.x;
-    const uint32_t p0 = crcdev::lds32(red + 4 * q), p1 = crcdev::lds32(red + 4 * (NR + q));
-    const uint32_t p2 = crcdev::lds32(red + 4 * (2 * NR + q)), p3 = crcdev::lds32(red + 4 * (3 * NR + q));
-    const uint32_t a = crcdev::zmap(p0, lev + 512u * 6) ^ p1;
-    const uint32_t b = crcdev::zmap(p2, lev + 512u * 6) ^ p3;
-    dst[q] = crcdev::zmap(a, lev + 512u * 7) ^ b;
-  }
-  __syncthreads();
-}
-
-// Run partials of object o from tile `tile` on, rows row0.. (ec_crc.hpp layout).
-__device__ __forceinline__ uint32_t* crc_part_at(const EncodeParams& p, uint32_t o, uint32_t tile) {
-  const uint64_t total = p.tiles * p.tile_ch + p.edge_tiles;
-  return p.crc_part + (static_cast<uint64_t>(o) * total + tile) * p.m + p.row0;
-}
-
-// Interior with the parity CRC: block b streams the contiguous items
-// [n*b/G, n*(b+1)/G) (ec_crc.hip run_begin), otherwise as encode_interior.
-template <class F, int K, int NR, bool DATA, bool NTL = false>
-__device__ __forceinline__ void encode_crc_interior(const EncodeParams& p) {
-  constexpr int NB = stream_bufs<K>();
-  constexpr uint32_t base = crc_lds_base<F, K>();
-  const uint64_t n = static_cast<uint64_t>(p.n_obj) * p.tiles;
-  // The 64-bit divisions are expanded into VALU code, so their results sit in
-  // VGPRs; without readfirstlane every buffer access whose soffset derives
-  // from them was wrapped in a waterfall loop (24 of them per item at k = 10,
-  // found round 3 in the generated code).
-  const IBlock ib = interior_block(p.edge_blocks);
-  const uint32_t begin = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n * ib.b / ib.g));
-  const uint32_t end = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n * (ib.b + 1) / ib.g));
-  uint32_t w = begin;
-  if (w >= end) return;
-  uint32_t o, x;
-  enc_item_pos(p, w, o, x);
-  uint32_t run0 = w - o * p.tiles;  // first tile of the current run
-  Rsrc cur = rsrc(p.objs + static_cast<uint64_t>(o) * p.obj_stride);
-  const uint32_t lane16 = lane_id() * 16;
-  constexpr int KP = stream_slots<K, NB>();
-  uint4 buf[NB];
-  // prologue shaped like the back edge (see encode_interior, HEAD)
-  const Rsrc none = rsrc(p.parity, 0);
-  const uint4 zero4 = make_uint4(0, 0, 0, 0);
-#pragma unroll
-  for (int j = 0; j < NB; ++j) {
-    if constexpr (DATA)
-      if (KP - NB + j < K) buf_st(none, lane16, 0, zero4);
-    if (j < K) buf[j] = buf_ld<!NTL>(cur, lane16, j * p.bs + x);
-  }
-#pragma unroll
-  for (int q = 0; q < NR; ++q) buf_st(none, lane16, 0, zero4);
-  uint32_t acc[NR];
-#pragma unroll
-  for (int q = 0; q < NR; ++q) acc[q] = 0;
-  // one item per trip: hipcc would otherwise unroll the item loop for small k
-  // (k = 2..6: 256 VGPRs unconstrained, up to 1.4 KB per lane of spills at 64)
-#pragma clang loop unroll(disable)
-  while (true) {
-    const uint32_t wn = w + 1 < end ? w + 1 : w;
-    uint32_t on, xn;
-    enc_item_pos(p, wn, on, xn);
-    const Rsrc nxt = rsrc(p.objs + static_cast<uint64_t>(on) * p.obj_stride, wn == w ? 0 : -1);
-    Rsrc dat;
-    if constexpr (DATA) dat = rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride);
-    typename F::Acc s;
-    F::zero(s);
-#pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      if (j < K) {
-        F::template mac<true>(F::kb(0), j * F::kTableBytes, buf[j % NB], s);
-        if constexpr (DATA) buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x, buf[j % NB]);
-      }
-      if (j + NB < KP) {
-        if (j + NB < K) buf[j % NB] = buf_ld<!NTL>(cur, lane16, (j + NB) * p.bs + x);
-      } else if (j + NB - KP < K) {
-        buf[j % NB] = buf_ld<!NTL>(nxt, lane16, (j + NB - KP) * p.bs + xn);
-      }
-    }
-    F::pin(s);
-    const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
-    const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x;
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      const uint4 v = F::row(s, q);
-      buf_st(par, lane16, soff + q * p.frag_stride, v);
-      acc[q] = crcdev::zmap(acc[q], base + kCrcZ4096) ^ crcdev::raw16(v, base);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (wn == w || on != o) {  // the run ends: object boundary or the block's last item
-      crc_block_flush<NR>(acc, base, crc_part_at(p, o, run0));
-      run0 = 0;
-    }
-    if (wn == w) break;
-    w = wn;
-    o = on;
-    x = xn;
-    cur = nxt;
-  }
-}
-
-// NTL: nontemporal input loads (A/B).
-template <class F, int K, int NR, bool DATA = false, bool NTL = false>
-__global__ void __launch_bounds__(kThreadsPerBlock)
-    __attribute__((amdgpu_waves_per_eu(DATA ? kEncodeCrcDataOcc
-                                            : (stream_bufs<K>() >= 6 ? 6 : kEncodeCrcOcc),
-                                       8)))
-    encode_crc_kernel(EncodeParams p) {
-  load_tables(p.tables, K * F::kTableBytes, 0);
-  load_tables(static_cast<const uint32_t*>(p.crc_tables), kCrcLdsBytes, crc_lds_base<F, K>());
-  __syncthreads();
-  // headers and edge items as encode_kernel; the edge tiles' CRC is taken by
-  // crc_finish_kernel from the parity just written
-  if (p.edge_blocks == 0) {
-    encode_edges<F, K, NR, DATA>(p, gridDim.x - 1 - blockIdx.x, gridDim.x);
-  } else if (blockIdx.x < p.edge_blocks) {
-    encode_edges<F, K, NR, DATA>(p, blockIdx.x, p.edge_blocks);
-    return;
-  }
-  encode_crc_interior<F, K, NR, DATA, NTL>(p);
-}
-
-// The parity CRC fused into the loader / consumer encode (encode_dma_kernel's
-// shape, W waves, W KiB items).  Block b streams the contiguous items
-// [N b / G, N (b + 1) / G) (crc_finish_kernel cuts the runs there), so a
-// thread's consecutive pieces of a parity payload are W KiB apart: acc =
-// Z_{W KiB}(acc) ^ raw16(piece).  A run's flush joins each wave's 64 lanes
-// with the lane tree (Z_16 .. Z_512) and the W waves with Z_1024 .. Z_8192,
-// and stores one raw CRC per row at the run's first 4 KiB tile.
-// DEFER: an item's CRC steps (per row: the Horner shift, then 4 dwords of
-// raw16 lookups) are spread over the next item's K slots instead of running
-// all at once after its last input -- every wave waits at each slot's barrier,
-// so a burst of lookups there leaves the ring without new loads; the item
-// that ends a run takes its steps at once, before the flush.  Measured
-// (tools/ab_bench.py --crc, same process, profiles/r04k_ab_crc.txt): W = 16
-// 336.7 us, W = 12 347.5, deferred steps 338.4 / 349.8, the stream CRC
-// kernel 343.2 (plain encode 266.9 on that box): the default is W = 16.
-// DATA (full stripe): each input chunk is stored to its data fragment from
-// the ring, and its raw CRC joins that fragment's accumulator in the same slot
-// (40 lookups per slot, no burst); the flush joins the k data rows too and
-// stores their run partials in crc_part_data, which the finishing pass turns
-// into the data fragments' header CRCs -- no separate CRC pass re-reads them.
-constexpr uint32_t kCrcZ8192 = offsetof(CrcTables, z8192);
-constexpr uint32_t kCrcZ12288 = offsetof(CrcTables, z12288);
-constexpr uint32_t kCrcZ16384 = offsetof(CrcTables, z16384);
-template <class F, int K, int R, int W = 16>
-__host__ __device__ constexpr uint32_t crc_dma_lds_bytes() {
-  // GF tables, CRC maps, W waves x (4 parity + K data rows) of partials, the ring
-  return crc_lds_base<F, K>() + ((kCrcLdsBytes + W * (4 + K) * 4 + 255u) & ~255u) + R * 1024u * W;
-}
-// CRC step u of a row set: u = 5 q is row q's Horner shift, 5 q + 1 + d its
-// dword d of raw16.
-template <int NR>
-__device__ __forceinline__ void crc_step(int u, uint32_t (&acc)[NR], const uint4 (&rows)[NR],
-                                         uint32_t base, uint32_t zshift) {
-  const int q = u / 5, d = u % 5 - 1;
-  if (d < 0) {
-    acc[q] = crcdev::zmap(acc[q], base + zshift);
-  } else {
-    const uint32_t w = d == 0 ? rows[q].x : d == 1 ? rows[q].y : d == 2 ? rows[q].z : rows[q].w;
-    acc[q] ^= crcdev::raw_dword(w, d, base);
-  }
-}
-template <class F, int K, int NR, int R, bool NT, bool DATA = false, int W = 16, bool DEFER = false>
-__global__ void __launch_bounds__(W * 64) encode_crc_dma_kernel(EncodeParams p) {
-  static_assert(W == 12 || W == 16, "12 or 16 waves");
-  constexpr int L = 4;
-  constexpr uint32_t kSlot = 1024u * W;
-  constexpr int kPerLoader = W / L;
-  constexpr uint32_t base = crc_lds_base<F, K>();
-  constexpr uint32_t red = base + kCrcLdsBytes;
-  constexpr uint32_t kRing = crc_dma_lds_bytes<F, K, R, W>() - R * kSlot;
-  constexpr uint32_t kZItem = W == 16 ? kCrcZ16384 : kCrcZ12288;
-  constexpr int kSteps = 5 * NR;
-  constexpr int KD = DATA ? K : 0;  // data-fragment CRC rows
-  constexpr uint32_t kRows = 4 + KD;  // partials per wave in `red`
-  load_tables(p.tables, K * F::kTableBytes, 0);
-  load_tables(static_cast<const uint32_t*>(p.crc_tables), kCrcLdsBytes, base);
-  __syncthreads();
-  if (blockIdx.x < p.edge_blocks) {  // edge items and headers: 256 threads
-    if (threadIdx.x >= kThreadsPerBlock) return;
-    encode_edges<F, K, NR, DATA>(p, blockIdx.x, p.edge_blocks);
-    return;
-  }
-  const uint32_t wave = wave_in_block(), lane = lane_id();
-  const uint64_t nall = static_cast<uint64_t>(p.n_obj) * p.tiles;
-  const IBlock ib = interior_block(p.edge_blocks);
-  const uint32_t begin = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nall * ib.b / ib.g));
-  const uint32_t end = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(nall * (ib.b + 1) / ib.g));
-  if (begin >= end) return;  // block-uniform
-  const uint32_t n_items = end - begin;
-  const bool loader = wave < static_cast<uint32_t>(L);
-  const uint32_t lane16 = lane * 16;
-  auto item_at = [&](uint32_t i, uint32_t& o, uint32_t& x0) {
-    const uint32_t w = begin + (i < n_items ? i : 0);
-    o = to_sgpr(w / p.tiles);
-    x0 = (w - o * p.tiles) * kSlot;
-  };
-  auto issue = [&](uint32_t i, int j, uint32_t ri) {
-    if (!loader) return;
-    uint32_t o, x0;
-    item_at(i, o, x0);
-    const v4u_s src = rsrc4(p.objs + static_cast<uint64_t>(o) * p.obj_stride, i < n_items ? ~0u : 0u);
-    const uint32_t part = wave * (kSlot / L);
-    const uint32_t lds = kRing + ri * kSlot + part;
-    const uint32_t soff = to_sgpr(j * p.bs + x0 + part);
-#pragma unroll
-    for (int c = 0; c < kPerLoader; ++c) dma16<NT>(src, lane16, soff + 1024 * c, lds + 1024 * c);
-  };
-#pragma unroll
-  for (int t = 0; t < R - 1; ++t) issue(t / K, t % K, t);
-  uint32_t ring = 0;
-  uint32_t o0, x00;
-  item_at(0, o0, x00);
-  uint32_t run0 = x00 / kTile;  // first 4 KiB tile of the current run
-  uint32_t acc[NR];
-  uint32_t accd[KD > 0 ? KD : 1];  // data fragments' raw CRCs (DATA)
-#pragma unroll
-  for (int j = 0; j < KD; ++j) accd[j] = 0;
-  uint4 prev[NR];  // DEFER: the previous item's rows, their CRC steps pending
-#pragma unroll
-  for (int q = 0; q < NR; ++q) {
-    acc[q] = 0;
-    prev[q] = make_uint4(0, 0, 0, 0);
-  }
-  bool pending = false;
-#pragma clang loop unroll(disable)
-  for (uint32_t i = 0; i < n_items; ++i) {
-    uint32_t o, x0;
-    item_at(i, o, x0);
-    const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
-    Rsrc dat;
-    if constexpr (DATA) dat = rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride);
-    typename F::Acc s;
-    F::zero(s);
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      if (loader) wait_vm<kPerLoader * (R - 2)>();
-      ring_barrier();
-      const uint32_t rn = ring == 0 ? R - 1 : ring - 1;
-      issue(i + (j + R - 1) / K, (j + R - 1) % K, rn);
-      const v4u xin = *lds_v4(kRing + ring * kSlot + wave * 1024 + lane16);
-      const uint4 x = make_uint4(xin.x, xin.y, xin.z, xin.w);
-      F::template mac<true>(F::kb(0), j * F::kTableBytes, x, s);
-      if constexpr (DATA) {
-        buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x0 + wave * 1024, x);
-        accd[j] = crcdev::zmap(accd[j], base + kZItem) ^ crcdev::raw16(x, base);
-      }
-      if constexpr (DEFER) {
-        if (pending) {  // the previous item's CRC steps [K j / .., K (j + 1) / ..)
-#pragma unroll
-          for (int u = j * kSteps / K; u < (j + 1) * kSteps / K; ++u) crc_step<NR>(u, acc, prev, base, kZItem);
-        }
-      }
-      ring = ring + 1 == R ? 0 : ring + 1;
-    }
-    F::pin(s);
-    const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x0 + wave * 1024;
-    uint4 rows[NR];
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      rows[q] = F::row(s, q);
-      buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, rows[q]);
-    }
-    uint32_t on, xn;
-    item_at(i + 1, on, xn);
-    const bool run_end = i + 1 == n_items || on != o;  // object boundary or the block's last item
-    if (!DEFER || run_end) {
-#pragma unroll
-      for (int q = 0; q < NR; ++q) {
-        acc[q] = crcdev::zmap(acc[q], base + kZItem) ^ crcdev::raw16(rows[q], base);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      pending = false;
-    } else {
-#pragma unroll
-      for (int q = 0; q < NR; ++q) prev[q] = rows[q];
-      pending = true;
-    }
-    if (run_end) {
-      const uint32_t lev = base + kCrcLevel;
-#pragma unroll
-      for (int q = 0; q < NR; ++q) {
-        uint32_t a = acc[q];
-#pragma unroll
-        for (int l = 0; l < 6; ++l) {
-          const uint32_t other = __shfl_down(a, 1u << l, 64);
-          a = crcdev::zmap(a, lev + 512u * l) ^ other;
-        }
-        if (lane == 0)
-          *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
-              static_cast<uintptr_t>(red + 4 * (wave * kRows + q))) = a;
-        acc[q] = 0;
-      }
-#pragma unroll
-      for (int j = 0; j < KD; ++j) {
-        uint32_t a = accd[j];
-#pragma unroll
-        for (int l = 0; l < 6; ++l) {
-          const uint32_t other = __shfl_down(a, 1u << l, 64);
-          a = crcdev::zmap(a, lev + 512u * l) ^ other;
-        }
-        if (lane == 0)
-          *reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(
-              static_cast<uintptr_t>(red + 4 * (wave * kRows + 4 + j))) = a;
-        accd[j] = 0;
-      }
-      __syncthreads();
-      const uint32_t q = threadIdx.x < static_cast<uint32_t>(NR) ? threadIdx.x : 4 + threadIdx.x - NR;
-      if (threadIdx.x < static_cast<uint32_t>(NR + KD)) {
-        // row q: waves 2v, 2v+1 (1 KiB apart) -> pairs (2 KiB) -> quads (4 KiB) -> the item
-        constexpr int kPairs = W / 2, kQuads = W / 4;
-        uint32_t r2[kPairs];
-#pragma unroll
-        for (int v = 0; v < kPairs; ++v)
-          r2[v] = crcdev::zmap(crcdev::lds32(red + 4 * (2 * v * kRows + q)), lev + 512u * 6) ^
-                  crcdev::lds32(red + 4 * ((2 * v + 1) * kRows + q));
-        uint32_t r4[kQuads];
-#pragma unroll
-        for (int v = 0; v < kQuads; ++v) r4[v] = crcdev::zmap(r2[2 * v], lev + 512u * 7) ^ r2[2 * v + 1];
-        uint32_t all;
-        if constexpr (W == 16) {
-          const uint32_t a = crcdev::zmap(r4[0], base + kCrcZ4096) ^ r4[1];
-          const uint32_t b = crcdev::zmap(r4[2], base + kCrcZ4096) ^ r4[3];
-          all = crcdev::zmap(a, base + kCrcZ8192) ^ b;
-        } else {
-          all = crcdev::zmap(r4[0], base + kCrcZ8192) ^ crcdev::zmap(r4[1], base + kCrcZ4096) ^ r4[2];
-        }
-        if (q < 4) {
-          crc_part_at(p, o, run0)[q] = all;
-        } else {
-          const uint64_t total = p.tiles * p.tile_ch + p.edge_tiles;
-          p.crc_part_data[(static_cast<uint64_t>(o) * total + run0) * K + (q - 4)] = all;
-        }
-      }
-      __syncthreads();
-      run0 = 0;  // the next run starts at its object's first tile
     }
   }
   if (loader) wait_vm<0>();  // no DMA may land in LDS after the block ends
@@ -1819,6 +1491,9 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
     F::pin(s);
     if constexpr (MODE == kReconstruct) {
       buf_st(out, lane16, kHeaderBytes + x, F::row(s, 0));
+      if (p.crc_part != nullptr)  // inline_crc32: the chunk's raw CRC (launch_decode_mode)
+        crc_store(p.crc_part + static_cast<uint64_t>(o) * crc_chunks(p.tiles, p.tile_ch) + x / kChunkBytes,
+                  crcdev::chunk_crc(F::row(s, 0), 2 * table_slot_bytes(K, F::kW), lane_id() * 4));
     } else {
       const uint32_t e = d.n_out();
 #pragma unroll
@@ -1913,6 +1588,12 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
     __attribute__((amdgpu_waves_per_eu(NBX > 6 ? 4 : kDecodeOcc, 8))) decode_kernel(DecodeParams p) {
   Slots st{0xFFFFFFFFu, 1u};
   TablePre<F, K> pre;
+  if constexpr (MODE == kReconstruct) {
+    if (p.crc_lanes != nullptr) {  // block-uniform: the lane tables after the two table slots
+      load_tables(static_cast<const uint32_t*>(p.crc_lanes), kCrcLaneBytes, 2 * table_slot_bytes(K, F::kW));
+      __syncthreads();
+    }
+  }
   if (p.fused_edges) {
     if (p.edge_blocks == 0) {
       decode_edges<F, K, MODE>(p, gridDim.x - 1 - blockIdx.x, gridDim.x, st, pre);
@@ -2302,81 +1983,38 @@ inline void set_tiles(EncodeParams& p, int64_t room, uint32_t ch) {
   p.edge_tiles = (p.bs + kTile - 1) / kTile - p.tiles * ch;
 }
 
-// The inline_crc32 encode: one encode launch with the parity CRC fused, then
-// the finishing pass over the run partials.
-template <class F, int K, int NR, class Kern>
-hipError_t launch_encode_crc(EncodeParams p, Kern kern, int per_cu, uint32_t edge_items,
-                             hipStream_t stream) {
-  p.fused_edges = 1;
-  int grid = 0;
-  const hipError_t e = launch_edges_apart(kern, p, crc_lds_bytes<F, K>(), p.n_obj * p.tiles,
-                                          edge_items, stream, per_cu, false, &grid);
-  if (e != hipSuccess) return e;
+// inline_crc32: the finishing pass (ec_crc.hip) over `count` fragments of
+// every object whose chunk partials a launch has just stored.
+inline hipError_t crc_finish(uint8_t* frags, uint64_t frag_stride, uint64_t stripe_stride,
+                             const uint32_t* part, uint32_t part_rows, uint32_t part_row0,
+                             const void* lanes, const void* tables, uint32_t n_obj, uint32_t count,
+                             uint32_t bs, uint32_t chunks, hipStream_t stream) {
   CrcFinishParams fp{};
-  fp.parity = p.parity;
-  fp.frag_stride = p.frag_stride;
-  fp.stripe_stride = p.stripe_stride;
-  fp.part = p.crc_part;
-  fp.maps = p.crc_tables;
-  fp.tables = p.crc_finish_tables;
-  fp.n_obj = p.n_obj;
-  fp.m = p.m;
-  fp.row0 = p.row0;
-  fp.nrows = NR;
-  fp.bs = p.bs;
-  fp.tiles = p.tiles * p.tile_ch;
-  fp.edge_tiles = p.edge_tiles;
-  fp.grid = static_cast<uint32_t>(grid);
-  fp.tile_ch = p.tile_ch;
+  fp.frags = frags;
+  fp.frag_stride = frag_stride;
+  fp.stripe_stride = stripe_stride;
+  fp.part = part;
+  fp.part_rows = part_rows;
+  fp.part_row0 = part_row0;
+  fp.lanes = lanes;
+  fp.tables = tables;
+  fp.n_obj = n_obj;
+  fp.count = count;
+  fp.bs = bs;
+  fp.chunks = chunks;
   return launch_crc_finish(fp, stream);
 }
 
-// The inline_crc32 encode in the loader / consumer shape: edge blocks, one
-// 1024-thread block per CU over contiguous item ranges, then the finishing pass.
-template <class F, int K, int NR, bool DATA, int W = 12, bool DEFER = false>
-hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
-  if (DATA && (p.crc_part_data == nullptr || p.crc_data_fused == nullptr)) return hipErrorInvalidValue;
-  set_tiles(p, last_room(p.bs, p.obj_len, K), W / 4);
-  const auto kern = encode_crc_dma_kernel<F, K, NR, 3, true, DATA, W, DEFER>;
-  constexpr size_t lds = crc_dma_lds_bytes<F, K, 3, W>();
-  if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
-  const int cus = device_cus();
-  const uint32_t items = p.n_obj * p.tiles;
-  const uint32_t edge_items = std::max(p.n_obj * p.edge_tiles, p.headers ? p.n_obj : 0u);
-  const uint32_t e = (std::min<uint32_t>(edge_items, static_cast<uint32_t>(cus)) + 7u) & ~7u;
-  uint32_t g = std::min<uint32_t>(static_cast<uint32_t>(cus) & ~7u, std::max(items, 1u));
-  if (g >= 8) g &= ~7u;
-  p.edge_blocks = edge_items ? e : 0;
-  p.fused_edges = 1;
-  p.xcd_split = 0;
-  hipLaunchKernelGGL(kern, dim3(g + p.edge_blocks), dim3(W * 64), lds, stream, p);
-  hipError_t err = hipGetLastError();
-  if (err != hipSuccess) return err;
-  CrcFinishParams fp{};
-  fp.parity = p.parity;
-  fp.frag_stride = p.frag_stride;
-  fp.stripe_stride = p.stripe_stride;
-  fp.part = p.crc_part;
-  fp.maps = p.crc_tables;
-  fp.tables = p.crc_finish_tables;
-  fp.n_obj = p.n_obj;
-  fp.m = p.m;
-  fp.row0 = p.row0;
-  fp.nrows = NR;
-  fp.bs = p.bs;
-  fp.tiles = p.tiles * p.tile_ch;
-  fp.edge_tiles = p.edge_tiles;
-  fp.grid = g;
-  fp.tile_ch = p.tile_ch;
-  if ((err = launch_crc_finish(fp, stream)) != hipSuccess || !DATA) return err;
-  // the data fragments' headers from their run partials
-  fp.parity = p.data;
-  fp.part = p.crc_part_data;
-  fp.m = K;
-  fp.row0 = 0;
-  fp.nrows = K;
-  if ((err = launch_crc_finish(fp, stream)) == hipSuccess) *p.crc_data_fused = 1;
-  return err;
+// The parity rows' (and, with the full stripe, the data fragments') headers
+// of an inline_crc32 encode launch whose interior covered `chunks` KiB.
+template <int K>
+hipError_t encode_crc_finish(const EncodeParams& p, bool data, uint32_t chunks, hipStream_t stream) {
+  hipError_t e = crc_finish(p.parity + static_cast<uint64_t>(p.row0) * p.frag_stride, p.frag_stride,
+                            p.stripe_stride, p.crc_part, p.m, p.row0, p.crc_lanes,
+                            p.crc_finish_tables, p.n_obj, p.nrows, p.bs, chunks, stream);
+  if (e != hipSuccess || !data) return e;
+  return crc_finish(p.data, p.frag_stride, p.stripe_stride, p.crc_part_data, K, 0, p.crc_lanes,
+                    p.crc_finish_tables, p.n_obj, K, p.bs, chunks, stream);
 }
 
 // The loader / consumer encode (encode_dma_kernel): one W * 64-thread block
@@ -2392,10 +2030,11 @@ hipError_t launch_encode_crc_dma(EncodeParams p, hipStream_t stream) {
 // batches keep the stream kernel's 4 KiB items).
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
           bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0, int COMB = 0>
-hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream) {
+hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream, uint32_t* chunks = nullptr) {
   set_tiles(p, last_room(p.bs, p.obj_len, K), 1024u * W * SW / kTile);
+  if (chunks) *chunks = crc_chunks(p.tiles, p.tile_ch);
   const auto kern = encode_dma_kernel<F, K, NR, R, NT, L, SW, W, DATA, NOCOMP, CONTIG, RUNS, COMB>;
-  constexpr size_t lds = dma_lds_bytes<F, K, R, SW, W>();
+  const size_t lds = dma_lds_bytes<F, K, R, SW, W>(p.crc_lanes != nullptr);
   if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
   const int cus = device_cus();
   const uint32_t items = p.n_obj * p.tiles;
@@ -2417,31 +2056,7 @@ template <class F, int K, int NR>
 hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint32_t edge_items) {
   constexpr size_t lds = K * F::kTableBytes;
   const int per_cu = ab_knob("ECAMD_ENC_PER_CU", kEncodePerCu);
-  if (p.crc_tables != nullptr) {
-    const int crc_per_cu = ab_knob("ECAMD_CRC_PER_CU", kEncodePerCu);
-    if constexpr (K == 10 && NR == 4) {
-      const int cw = ab_knob("ECAMD_CRC_DMA_W", 16), defer = ab_knob("ECAMD_CRC_DEFER", 0);
-      if (cw == 12 && !defer)
-        return data ? launch_encode_crc_dma<F, K, NR, true, 12>(p, stream)
-                    : launch_encode_crc_dma<F, K, NR, false, 12>(p, stream);
-      if (cw == 16 && defer)
-        return data ? launch_encode_crc_dma<F, K, NR, true, 16, true>(p, stream)
-                    : launch_encode_crc_dma<F, K, NR, false, 16, true>(p, stream);
-      if (cw == 12 && defer)
-        return data ? launch_encode_crc_dma<F, K, NR, true, 12, true>(p, stream)
-                    : launch_encode_crc_dma<F, K, NR, false, 12, true>(p, stream);
-    }
-    if constexpr (K == 10 && NR == 4)
-      if (!data && ab_knob("ECAMD_CRC_NTL", 0))
-        return launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR, false, true>, crc_per_cu,
-                                           edge_items, stream);
-    if (crc_per_cu != kEncodePerCu)
-      return data ? launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR, true>, crc_per_cu,
-                                                edge_items, stream)
-                  : launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR>, crc_per_cu,
-                                                edge_items, stream);
-    return hipErrorNotSupported;
-  }
+  if (p.crc_lanes != nullptr) return hipErrorNotSupported;  // no A/B forms of the CRC encode
   if (ab_knob("ECAMD_EDGE_SIDE", 0)) {
     p.fused_edges = 0;
     hipError_t e = fork_join(
@@ -2516,8 +2131,9 @@ hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint3
 }
 
 // Encode: one launch -- interior stream + edge items + headers, and the data
-// fragments when asked (stored from the input registers) -- or, with
-// inline_crc32, the CRC-fused launch and its finishing pass.
+// fragments when asked (stored from the input registers); with inline_crc32
+// the same launch stores its chunks' CRC partials, and the finishing pass
+// follows.
 template <class F, int K, int NR>
 hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   const int64_t room = last_room(p.bs, p.obj_len, K);
@@ -2533,25 +2149,36 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   }
   if constexpr (kAB && F::kRows > kRowsPerPass) {  // eight-row encode: blocks per CU
     const int per_cu = ab_knob("ECAMD_ENC_PER_CU", kEncodePerCu);
-    if (per_cu != kEncodePerCu && !data && p.crc_tables == nullptr) {
+    if (per_cu != kEncodePerCu && !data && p.crc_lanes == nullptr) {
       p.fused_edges = 1;
       return launch_edges_apart(encode_kernel<F, K, NR>, p, lds, p.n_obj * p.tiles, edge_items,
                                 stream, per_cu, true);
     }
   }
-  if (p.crc_tables != nullptr) {
+  if (p.crc_lanes != nullptr) {
     if constexpr (F::kRows > kRowsPerPass) {
-      return hipErrorInvalidValue;  // the fused CRC runs in four-row passes
+      return hipErrorInvalidValue;  // the inline CRC runs in four-row passes
     } else {
+      uint32_t chunks = 0;
+      hipError_t e = hipSuccess;
+      bool dma = false;
       if constexpr (K >= kDmaMinK) {
-        if (dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) && !ab_knob("ECAMD_CRC_STREAM", 0))
-          return data ? launch_encode_crc_dma<F, K, NR, true, 16>(p, stream)
-                      : launch_encode_crc_dma<F, K, NR, false, 16>(p, stream);
+        dma = dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) && !ab_knob("ECAMD_CRC_STREAM", 0);
+        if (dma)
+          e = data ? launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream, &chunks)
+                   : launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream, &chunks);
       }
-      return data ? launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR, true>, kEncodePerCu,
-                                                edge_items, stream)
-                  : launch_encode_crc<F, K, NR>(p, encode_crc_kernel<F, K, NR>, kEncodePerCu,
-                                                edge_items, stream);
+      if (!dma) {
+        p.fused_edges = 1;
+        chunks = crc_chunks(p.tiles, p.tile_ch);
+        const size_t crc_lds = crc_lds_base<F, K>() + kCrcLaneBytes;
+        e = data ? launch_edges_apart(encode_kernel<F, K, NR, false, true, 1, false, 0, false, true>, p,
+                                      crc_lds, p.n_obj * p.tiles, edge_items, stream, kEncodePerCu, true)
+                 : launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, false, 0, false, true>, p,
+                                      crc_lds, p.n_obj * p.tiles, edge_items, stream, kEncodePerCu, true);
+      }
+      if (e != hipSuccess) return e;
+      return encode_crc_finish<K>(p, data, chunks, stream);
     }
   }
   // the loader / consumer encode (encode_dma_kernel) for k >= kDmaMinK; its
@@ -2568,22 +2195,6 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
                               stream, kEncodePerCu, true);
   return launch_edges_apart(encode_kernel<F, K, NR>, p, lds, items, edge_items, stream,
                             kEncodePerCu, true);
-}
-
-template <class F, int K>
-hipError_t launch_encode_rows(const EncodeParams& p, hipStream_t stream) {
-  switch (p.nrows) {
-    case 1:
-      return launch_encode_k<F, K, 1>(p, stream);
-    case 2:
-      return launch_encode_k<F, K, 2>(p, stream);
-    case 3:
-      return launch_encode_k<F, K, 3>(p, stream);
-    case 4:
-      return launch_encode_k<F, K, 4>(p, stream);
-    default:
-      return hipErrorInvalidValue;
-  }
 }
 
 // LDS of a decode launch: two table slots.
@@ -2687,6 +2298,19 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
     constexpr size_t lds = decode_lds_bytes<F, K>();
     const uint32_t edge_items =
         std::max(p.n_obj * p.edge_tiles, MODE == kReconstruct && p.headers ? p.n_obj : 0u);
+    // inline_crc32 reconstruct: the same launch with its chunks' partials,
+    // then the finishing pass (no A/B forms)
+    const bool crc = MODE == kReconstruct && p.crc_lanes != nullptr;
+    if (MODE != kReconstruct && p.crc_lanes != nullptr) return hipErrorInvalidValue;
+    if (crc) {
+      p.fused_edges = 1;
+      hipError_t e = launch_edges_apart(decode_kernel<F, K, MODE>, p, lds + kCrcLaneBytes,
+                                        p.n_obj * p.tiles, edge_items, stream, kReconstructPerCu,
+                                        kDecodeXcd);
+      if (e != hipSuccess) return e;
+      return crc_finish(p.out, 0, p.out_stride, p.crc_part, 1, 0, p.crc_lanes, p.crc_finish_tables,
+                        p.n_obj, 1, p.bs, crc_chunks(p.tiles, p.tile_ch), stream);
+    }
     if constexpr (kAB) {
       const hipError_t e = launch_decode_ab<F, K, MODE>(p, stream, edge_items);
       if (e != hipErrorNotSupported) return e;

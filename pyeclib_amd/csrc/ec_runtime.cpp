@@ -126,7 +126,6 @@ struct Knobs {
   int host_streams = 3;         // ECAMD_HOST_STREAMS
   int host_chunk_mb = 32;       // ECAMD_HOST_CHUNK_MB
   bool edge_blocks = true;      // ECAMD_EDGE_BLOCKS=0: the round-2 launch form
-  bool crc_fused = true;        // ECAMD_CRC_FUSED=0: parity CRC as a separate pass
   static Knobs from_env() {
     Knobs k;
     k.single_pinned_max = static_cast<size_t>(
@@ -137,7 +136,6 @@ struct Knobs {
     k.host_streams = static_cast<int>(env_long("ECAMD_HOST_STREAMS", k.host_streams));
     k.host_chunk_mb = static_cast<int>(std::max<long>(1, env_long("ECAMD_HOST_CHUNK_MB", k.host_chunk_mb)));
     k.edge_blocks = env_on("ECAMD_EDGE_BLOCKS", true);
-    k.crc_fused = env_on("ECAMD_CRC_FUSED", true);
     k.register_caller = env_on("ECAMD_REGISTER_CALLER", false);
     return k;
   }
@@ -361,9 +359,9 @@ struct Instance {
   hipStream_t hstream[kHostStreams] = {};  // host-resident pipeline
   DevBuf hbuf[kHostStreams];
   hipEvent_t hdone[kHostStreams] = {};
-  std::map<uint64_t, DevBuf> crc_tables;  // payload size -> CrcTables (device)
+  DevBuf crc_lanes;                       // CrcLaneTables (device), the instance's CRC variant
   std::map<uint64_t, DevBuf> crc_finish;  // payload size -> CrcFinishTables (device)
-  // fused parity CRC run partials, one buffer per launch stream: a launch
+  // inline_crc32 chunk partials, one buffer per launch stream: a launch
   // reads and writes its own stream's buffer, so launches on different
   // streams (the staged host pipeline deals chunks over 3) never share one
   // and need no device-wide wait between them
@@ -482,7 +480,7 @@ struct Instance {
     scratch.release();
     pin.release();
     for (auto& b : hbuf) b.release();
-    for (auto& kv : crc_tables) kv.second.release();
+    crc_lanes.release();
     for (auto& kv : crc_finish) kv.second.release();
     for (auto& c : crc_part) c.buf.release();
     if (stream) (void)hipStreamDestroy(stream);
@@ -952,6 +950,8 @@ struct DecodeJob {
   const uint8_t* headers;     // reconstruct: n_obj headers (host), else null
   bool compact = false;       // object o's i-th input (ascending fragment index)
                               // at frags + o*stripe_stride + i*frag_stride
+  bool crc = false;           // reconstruct with inline_crc32: the launch sets each
+                              // fragment's payload checksum (EncodeParams::crc_lanes)
 };
 
 // Descriptors of objects [o0, o1) of a job: `passes` arrays of (o1 - o0)
@@ -997,6 +997,10 @@ uint32_t passes_of(const DecodeJob& J, const DescBatch& B, int o0, int o1) {
   return std::max<uint32_t>(1, static_cast<uint32_t>((rows + kRowsPerPass - 1) / kRowsPerPass));
 }
 
+const void* crc_lanes_for(Instance& I, hipError_t* err);
+const void* crc_finish_for(Instance& I, uint64_t bs, hipError_t* err);
+size_t crc_part_bytes(int n_obj, uint64_t bs, int rows);
+
 // Launch the kernel passes for objects [o0, o1) whose descriptors (passes x
 // n ObjDesc, then headers) are at `dev`.
 hipError_t launch_range(Instance& I, const DecodeJob& J, int o0, int o1, uint32_t passes,
@@ -1004,8 +1008,19 @@ hipError_t launch_range(Instance& I, const DecodeJob& J, int o0, int o1, uint32_
   const int n = o1 - o0;
   if (hipError_t e = I.note_stream(stream); e != hipSuccess) return e;
   if (hipError_t e = pool_commit(I, stream); e != hipSuccess) return e;
+  const void* crc_lanes = nullptr;
+  const void* crc_fin = nullptr;
+  uint32_t* crc_part = nullptr;
+  if (J.crc) {
+    hipError_t e;
+    if (!(crc_lanes = crc_lanes_for(I, &e)) || !(crc_fin = crc_finish_for(I, bs, &e))) return e;
+    if ((e = crc_part_for(I, stream, crc_part_bytes(n, bs, 1), &crc_part)) != hipSuccess) return e;
+  }
   for (uint32_t p = 0; p < passes; ++p) {
     DecodeParams P{};
+    P.crc_lanes = crc_lanes;
+    P.crc_finish_tables = crc_fin;
+    P.crc_part = crc_part;
     P.frags = J.frags + static_cast<uint64_t>(o0) * J.stripe_stride;
     P.frag_stride = J.frag_stride;
     P.stripe_stride = J.stripe_stride;
@@ -1157,65 +1172,55 @@ int run_decode(Instance& I, const DecodeJob& J, hipStream_t stream) {
   return e2 == hipSuccess ? 0 : hip_errno(e2);
 }
 
-// Device copy of per-payload-size CRC tables (a bounded cache, ~9 KiB per
-// size: when full, wait for the instance's own launches -- its users -- then
-// drop it).  Returns null on failure (*err set).
+// inline_crc32 tables on the device (zlib's CRC, or the legacy one when the
+// instance writes legacy CRCs): the lane tables once per instance, the
+// finishing tables per payload size (a bounded cache, ~12 KiB per size:
+// when full, wait for the instance's own launches -- its users -- then drop
+// it).  Null on failure (*err set).
 constexpr size_t kCrcTableSizes = 64;
-template <class T, class Build>
-const void* crc_table_cache(Instance& I, std::map<uint64_t, DevBuf>& cache, uint64_t bs,
-                            Build build, hipError_t* err) {
+const void* crc_lanes_for(Instance& I, hipError_t* err) {
   *err = hipSuccess;
-  auto it = cache.find(bs);
-  if (it == cache.end()) {
-    if (cache.size() >= kCrcTableSizes) {
+  if (I.crc_lanes.p) return I.crc_lanes.p;
+  std::unique_ptr<CrcLaneTables> host(new CrcLaneTables);
+  build_crc_lane_tables(I.legacy_crc, host.get());
+  hipError_t e = I.crc_lanes.ensure(sizeof(CrcLaneTables));
+  if (e == hipSuccess) e = hipMemcpy(I.crc_lanes.p, host.get(), sizeof(CrcLaneTables), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    I.crc_lanes.release();
+    *err = e;
+    return nullptr;
+  }
+  return I.crc_lanes.p;
+}
+
+const void* crc_finish_for(Instance& I, uint64_t bs, hipError_t* err) {
+  *err = hipSuccess;
+  auto it = I.crc_finish.find(bs);
+  if (it == I.crc_finish.end()) {
+    if (I.crc_finish.size() >= kCrcTableSizes) {
       if ((*err = I.wait_streams()) != hipSuccess) return nullptr;
-      for (auto& kv : cache) kv.second.release();
-      cache.clear();
+      for (auto& kv : I.crc_finish) kv.second.release();
+      I.crc_finish.clear();
     }
-    std::unique_ptr<T> host(new T);
-    build(host.get());
+    std::unique_ptr<CrcFinishTables> host(new CrcFinishTables);
+    build_crc_finish_tables(static_cast<uint32_t>(bs), I.legacy_crc, host.get());
     DevBuf buf;
-    hipError_t e = buf.ensure(sizeof(T));
-    if (e == hipSuccess) e = hipMemcpy(buf.p, host.get(), sizeof(T), hipMemcpyHostToDevice);
+    hipError_t e = buf.ensure(sizeof(CrcFinishTables));
+    if (e == hipSuccess) e = hipMemcpy(buf.p, host.get(), sizeof(CrcFinishTables), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       buf.release();
       *err = e;
       return nullptr;
     }
-    it = cache.emplace(bs, buf).first;
+    it = I.crc_finish.emplace(bs, buf).first;
   }
   return it->second.p;
 }
 
-const void* crc_tables_for(Instance& I, uint64_t bs, hipError_t* err) {
-  const uint32_t steps = static_cast<uint32_t>((bs + 4095) / 4096);
-  return crc_table_cache<CrcTables>(
-      I, I.crc_tables, bs,
-      [&](CrcTables* t) { build_crc_tables(static_cast<uint32_t>(bs), steps, t); }, err);
-}
-
-// Inline CRC-32 of `count` fragments per object (caller holds I.mu): payload
-// checksum and metadata checksum patched into headers already written.
-int run_crc(Instance& I, uint8_t* base, uint64_t frag_stride, uint64_t stripe_stride,
-            uint32_t count, int n_obj, uint64_t bs, hipStream_t stream) {
-  if (bs == 0 || n_obj == 0 || count == 0) return 0;
-  const uint32_t steps = static_cast<uint32_t>((bs + 4095) / 4096);
-  hipError_t te;
-  const void* tables = crc_tables_for(I, bs, &te);
-  if (!tables) return hip_errno(te);
-  CrcParams P{};
-  P.frags = base;
-  P.frag_stride = frag_stride;
-  P.stripe_stride = stripe_stride;
-  P.first = 0;
-  P.count = count;
-  P.n_obj = static_cast<uint32_t>(n_obj);
-  P.bs = static_cast<uint32_t>(bs);
-  P.steps = steps;
-  P.tables = tables;
-  hipError_t e = I.note_stream(stream);
-  if (e == hipSuccess) e = launch_crc(P, stream);
-  return e == hipSuccess ? 0 : hip_errno(e);
+// 1 KiB chunk partials of `rows` fragments per object (the launches store at
+// most bs / 1024 chunks per fragment).
+size_t crc_part_bytes(int n_obj, uint64_t bs, int rows) {
+  return static_cast<size_t>(n_obj) * (bs / 1024 + 1) * rows * sizeof(uint32_t);
 }
 
 int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t obj_len, int n_obj,
@@ -1235,9 +1240,8 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
   Upload u;
   hipError_t e;
   if (headers) {
-    // the GPU CRC writes zlib crc32 only; the legacy variant stays host-side
-    if (I.ct == CHKSUM_CRC32 && I.legacy_crc) return -EBACKENDNOTSUPP;
-    // headers depend only on (obj_len) for a given instance
+    // headers depend only on (obj_len) for a given instance; with
+    // inline_crc32 their chksum[0] is 0 here and the finishing pass sets it
     std::vector<uint8_t> key;
     key_append(key, &obj_len, 1);
     int rc = upload(I, I.hdr_cache, key, 0, hdr_bytes, stream,
@@ -1250,48 +1254,38 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
                     &u);
     if (rc < 0) return rc;
   }
-  // inline_crc32: the parity CRC fused into the encode launch
-  // (knob ECAMD_CRC_FUSED=0: the separate CRC pass, as for data fragments)
+  // inline_crc32: every launch stores its chunks' CRC partials, and the
+  // launcher runs the finishing pass (parity rows; data fragments too)
   const bool crc = headers && I.ct == CHKSUM_CRC32 && bs > 0;
-  const bool fused_crc = crc && I.knobs.crc_fused;
-  const void* crc_maps = nullptr;
+  const void* crc_lanes = nullptr;
   const void* crc_fin = nullptr;
   uint32_t* crc_part = nullptr;
   if ((e = I.note_stream(stream)) != hipSuccess) {
     (void)upload_done(I, u, stream);
     return hip_errno(e);
   }
-  if (fused_crc) {
-    const uint32_t total = static_cast<uint32_t>((bs + 4095) / 4096);
+  if (crc) {
     hipError_t te;
-    if (!(crc_maps = crc_tables_for(I, bs, &te)) ||
-        !(crc_fin = crc_table_cache<CrcFinishTables>(
-              I, I.crc_finish, bs,
-              [&](CrcFinishTables* t) { build_crc_finish_tables(static_cast<uint32_t>(bs), total, t); },
-              &te))) {
+    if (!(crc_lanes = crc_lanes_for(I, &te)) || !(crc_fin = crc_finish_for(I, bs, &te))) {
       (void)upload_done(I, u, stream);
       return hip_errno(te);
     }
     // parity partials, then room for the data fragments' (full stripe)
-    const size_t part_bytes = static_cast<size_t>(n_obj) * total * (m + (data ? k : 0)) * sizeof(uint32_t);
-    if ((e = crc_part_for(I, stream, part_bytes, &crc_part)) != hipSuccess) {
+    if ((e = crc_part_for(I, stream, crc_part_bytes(n_obj, bs, m + (data ? k : 0)), &crc_part)) !=
+        hipSuccess) {
       (void)upload_done(I, u, stream);
       return hip_errno(e);
     }
   }
-  uint32_t data_crc_fused = 0;  // set by the launcher (EncodeParams::crc_data_fused)
-  // one eight-row pass for 4 < m <= 8 (the fused CRC keeps four-row passes)
-  const bool wide = I.wide && !fused_crc;
+  // one eight-row pass for 4 < m <= 8 (the inline CRC keeps four-row passes)
+  const bool wide = I.wide && !crc;
   const uint32_t passes = wide ? 1 : I.passes;
   for (uint32_t p = 0; p < passes; ++p) {
     EncodeParams P{};
-    P.crc_tables = crc_maps;
+    P.crc_lanes = crc_lanes;
     P.crc_finish_tables = crc_fin;
     P.crc_part = crc_part;
-    if (fused_crc && data) {
-      P.crc_part_data = crc_part + static_cast<size_t>(n_obj) * ((bs + 4095) / 4096) * m;
-      P.crc_data_fused = &data_crc_fused;
-    }
+    if (crc && data) P.crc_part_data = crc_part + crc_part_bytes(n_obj, bs, m) / sizeof(uint32_t);
     P.objs = objs;
     P.obj_stride = obj_stride;
     P.obj_len = obj_len;
@@ -1320,12 +1314,6 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
     }
   }
   if ((e = upload_done(I, u, stream)) != hipSuccess) return hip_errno(e);
-  if (headers && I.ct == CHKSUM_CRC32) {
-    int rc = fused_crc ? 0 : run_crc(I, parity, frag_stride, stripe_stride, m, n_obj, bs, stream);
-    if (rc == 0 && data && !data_crc_fused)
-      rc = run_crc(I, data, frag_stride, stripe_stride, k, n_obj, bs, stream);
-    if (rc < 0) return rc;
-  }
   return 0;
 }
 
@@ -2189,7 +2177,6 @@ int ecamd_reconstruct_batch(int desc, const void* d_frags, uint64_t frag_stride,
   auto I = lookup(desc);
   if (!I) return -EBACKENDNOTAVAIL;
   if (n_obj == 0) return 0;
-  if (I->ct == CHKSUM_CRC32 && I->legacy_crc) return -EBACKENDNOTSUPP;
   std::lock_guard<std::mutex> lk(I->mu);
   DeviceGuard g(I->device);
   CallScope cs(*I);
@@ -2202,11 +2189,8 @@ int ecamd_reconstruct_batch(int desc, const void* d_frags, uint64_t frag_stride,
   }
   DecodeJob J{static_cast<const uint8_t*>(d_frags), frag_stride, stripe_stride, obj_len,
               static_cast<uint8_t*>(d_out), out_stride, n_obj, h_avail, h_dest, hdr.data()};
-  int rc = run_decode(*I, J, static_cast<hipStream_t>(stream));
-  if (rc == 0 && I->ct == CHKSUM_CRC32)
-    rc = run_crc(*I, static_cast<uint8_t*>(d_out), 0, out_stride, 1, n_obj, bs,
-                 static_cast<hipStream_t>(stream));
-  return rc;
+  J.crc = I->ct == CHKSUM_CRC32 && bs > 0;
+  return run_decode(*I, J, static_cast<hipStream_t>(stream));
 }
 
 int ecamd_encode_host_batch(int desc, const void* h_objs, uint64_t obj_stride, uint64_t obj_len,
@@ -2263,7 +2247,6 @@ int ecamd_reconstruct_host_batch(int desc, const void* h_frags, uint64_t frag_st
   auto I = lookup(desc);
   if (!I) return -EBACKENDNOTAVAIL;
   if (n_obj == 0) return 0;
-  if (I->ct == CHKSUM_CRC32 && I->legacy_crc) return -EBACKENDNOTSUPP;
   const uint64_t bs = blocksize_of(I->k, I->code.w, obj_len);
   if (obj_len == 0 || frag_stride % 16 || out_stride % 16 ||
       frag_stride < kHeaderBytes + round16(bs) || out_stride < kHeaderBytes + round16(bs))
@@ -2284,10 +2267,8 @@ int ecamd_reconstruct_host_batch(int desc, const void* h_frags, uint64_t frag_st
                                          hipStream_t s) {
     DecodeJob J{d_in, frag_stride, gs, obj_len, d_out, out_stride, n, h_avail + o0,
                 h_dest + o0, hdr.data() + static_cast<size_t>(o0) * kHeaderBytes, true};
-    int rc = run_decode(*I, J, s);
-    if (rc == 0 && I->ct == CHKSUM_CRC32)
-      rc = run_crc(*I, d_out, 0, out_stride, 1, n, bs, s);
-    return rc;
+    J.crc = I->ct == CHKSUM_CRC32 && bs > 0;
+    return run_decode(*I, J, s);
   });
 }
 

@@ -1,0 +1,115 @@
+// Host restatement of the GPU inline-CRC scheme (crc_device.hpp chunk_crc,
+// ec_crc.hip crc_finish_kernel), checked against the byte-serial CRCs.
+// Built and run by tests/test_crc_math.py with g++ against
+// pyeclib_amd/csrc/crc32.cpp -- no GPU, no HIP.
+//
+// For payload sizes around the chunk and tile boundaries, in both variants
+// (zlib and liberasurecode's legacy CRC) and for several interior chunk
+// counts: the 1 KiB chunks' raw CRCs from the lane tables, shifted to the
+// payload's end as the finishing pass does, plus the end-aligned edge
+// chunks, plus the init term, must equal crc32 / crc32_legacy of the
+// payload; and the metadata checksum patched by the linear delta must equal
+// the checksum recomputed over the patched header.
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "crc32.hpp"
+
+using namespace ecamd;
+
+static uint32_t zmap(const uint32_t (*t)[16], uint32_t r) {
+  uint32_t a = 0;
+  for (int q = 0; q < 8; ++q) a ^= t[q][(r >> (4 * q)) & 15];
+  return a;
+}
+
+static uint32_t raw16(const CrcLaneTables& L, const uint8_t* b) {
+  uint32_t a = 0;
+  for (int i = 0; i < 16; ++i) a ^= L.raw16[2 * i][b[i] & 15] ^ L.raw16[2 * i + 1][b[i] >> 4];
+  return a;
+}
+
+static uint32_t lane_map(const CrcLaneTables& L, uint32_t r, int lane) {
+  uint32_t a = 0;
+  for (int q = 0; q < 8; ++q) a ^= L.lane[q][(r >> (4 * q)) & 15][lane];
+  return a;
+}
+
+// chunk_crc: 64 lanes x 16 bytes
+static uint32_t chunk_crc(const CrcLaneTables& L, const uint8_t* c) {
+  uint32_t a = 0;
+  for (int l = 0; l < 64; ++l) a ^= lane_map(L, raw16(L, c + 16 * l), l);
+  return a;
+}
+
+static uint32_t shift_chunks(const CrcFinishTables& F, uint32_t r, uint32_t d) {
+  for (int i = 0; d; ++i, d >>= 1)
+    if (d & 1) r = zmap(F.pow[i], r);
+  return r;
+}
+
+// the finishing pass for one payload, interior = chunks [0, chunks)
+static uint32_t finish(const CrcLaneTables& L, const CrcFinishTables& F, const uint8_t* pay,
+                       uint32_t bs, uint32_t chunks) {
+  const uint32_t nfull = bs / 1024;
+  uint32_t acc = 0;
+  for (uint32_t c = 0; c < chunks; ++c) acc ^= shift_chunks(F, chunk_crc(L, pay + 1024 * c), nfull - 1 - c);
+  const int64_t e0 = int64_t(chunks) * 1024;
+  const uint32_t n_edge = static_cast<uint32_t>((int64_t(bs) - e0 + 1023) / 1024);
+  uint32_t edge = 0;
+  for (uint32_t j = 0; j < n_edge; ++j) {
+    uint8_t buf[1024];
+    const int64_t start = int64_t(bs) - 1024 * int64_t(j + 1);
+    for (int b = 0; b < 1024; ++b) {
+      const int64_t at = start + b;
+      buf[b] = (at >= e0 && at < int64_t(bs)) ? pay[at] : 0;
+    }
+    edge ^= shift_chunks(F, chunk_crc(L, buf), j);
+  }
+  return zmap(F.zr, acc) ^ edge ^ F.init_term;
+}
+
+int main() {
+  std::mt19937_64 rng(20261018);
+  int failures = 0, checks = 0;
+  CrcLaneTables* L = new CrcLaneTables;
+  CrcFinishTables* F = new CrcFinishTables;
+  const uint32_t sizes[] = {1, 2, 15, 16, 17, 1000, 1023, 1024, 1025, 2048, 4095, 4096, 4097,
+                            12287, 12288, 12289, 16384, 20000, 104864, 419432};
+  for (int legacy = 0; legacy < 2; ++legacy) {
+    build_crc_lane_tables(legacy != 0, L);
+    for (uint32_t bs : sizes) {
+      build_crc_finish_tables(bs, legacy != 0, F);
+      std::vector<uint8_t> pay(bs);
+      for (auto& b : pay) b = static_cast<uint8_t>(rng());
+      const uint32_t want = legacy ? crc32_legacy(0, pay.data(), bs) : crc32(0, pay.data(), bs);
+      // interior chunk counts: none, one, all 4 KiB tiles, every full chunk
+      const uint32_t cands[] = {0u, bs >= 1024 ? 1u : 0u, bs / 4096 * 4, bs / 1024};
+      for (uint32_t chunks : cands) {
+        ++checks;
+        const uint32_t got = finish(*L, *F, pay.data(), bs, chunks);
+        if (got != want) {
+          ++failures;
+          std::printf("FAIL legacy=%d bs=%u chunks=%u got %08x want %08x\n", legacy, bs, chunks, got, want);
+        }
+      }
+      // metadata checksum: delta from chksum[0] = 0 to chksum[0] = want
+      uint8_t h[80];
+      for (auto& b : h) b = static_cast<uint8_t>(rng());
+      std::memset(h + 21, 0, 4);
+      const uint32_t m0 = legacy ? crc32_legacy(0, h, 59) : crc32(0, h, 59);
+      std::memcpy(h + 21, &want, 4);
+      const uint32_t m1 = legacy ? crc32_legacy(0, h, 59) : crc32(0, h, 59);
+      ++checks;
+      if ((m0 ^ zmap(F->meta, want)) != m1) {
+        ++failures;
+        std::printf("FAIL meta legacy=%d bs=%u\n", legacy, bs);
+      }
+    }
+  }
+  std::printf("%d checks, %d failures\n", checks, failures);
+  return failures ? 1 : 0;
+}

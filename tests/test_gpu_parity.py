@@ -295,15 +295,32 @@ def test_isal_cauchy_batch(oracle, gpu, k, m, obj_len):
     ("amd_rs_vand", 10, 4, 4 * 1024 * 1024, 3), ("amd_rs_vand", 4, 2, 100001, 3),
     ("amd_rs_vand", 12, 2, 4096 * 12 * 2, 3), ("amd_rs_vand", 3, 1, 17, 3),
     ("isa_l_rs_cauchy", 12, 4, 999999, 3), ("isa_l_rs_vand", 8, 4, 65537, 3),
-    # fused parity CRC: runs of many tiles cut at block and object boundaries
-    # (the grid is far smaller than the item list), multi-pass parity (m > 4)
+    # many objects per launch (the loader / consumer kernels; the stream
+    # kernels take the small batches above), multi-pass parity (m > 4)
     ("amd_rs_vand", 10, 4, 4 * 1024 * 1024, 160), ("amd_rs_vand", 6, 6, 300000, 40),
     ("isa_l_rs_cauchy", 12, 4, 3 * 1024 * 1024 + 5, 48)])
 def test_batch_inline_crc32(oracle, gpu, ec_type, k, m, obj_len, n_obj):
     """chksum_type inline_crc32 on device-resident batches: every header
     (payload CRC-32 + metadata checksum) equals the oracle's, for encode with
-    data fragments and for reconstruct.  The parity CRC is fused into the
-    encode launch; data fragments and reconstruct use the CRC pass."""
+    data fragments, encode of the parity alone, and reconstruct.  Each launch
+    stores its 1 KiB chunks' CRCs and a finishing pass sets the headers
+    (ec_crc.hip); no pass re-reads the payloads."""
+    _check_batch_crc(oracle, gpu, ec_type, k, m, obj_len, n_obj, legacy=False)
+
+
+@pytest.mark.parametrize("ec_type,k,m,obj_len,n_obj", [
+    ("amd_rs_vand", 10, 4, 1 << 20, 5), ("amd_rs_vand", 10, 4, 4 * 1024 * 1024, 12),
+    ("amd_rs_vand", 6, 6, 300001, 4), ("isa_l_rs_vand", 8, 4, 65537, 3)])
+def test_batch_legacy_crc32(oracle, gpu, monkeypatch, ec_type, k, m, obj_len, n_obj):
+    """LIBERASURECODE_WRITE_LEGACY_CRC=1: the batch encode and reconstruct
+    write liberasurecode's legacy CRC (liberasurecode_crc32_alt) into the
+    payload and metadata checksums, as the reference path does in every call
+    (pyeclib_c.c:248)."""
+    monkeypatch.setenv("LIBERASURECODE_WRITE_LEGACY_CRC", "1")
+    _check_batch_crc(oracle, gpu, ec_type, k, m, obj_len, n_obj, legacy=True)
+
+
+def _check_batch_crc(oracle, gpu, ec_type, k, m, obj_len, n_obj, legacy):
     import torch
     from pyeclib_amd import batch
     codec = batch.BatchCodec(k, m, inline_crc32=True, ec_type=ec_type)
@@ -322,8 +339,15 @@ def test_batch_inline_crc32(oracle, gpu, ec_type, k, m, obj_len, n_obj):
             want = oracle.isal_encode(kind, k, m, data, ct=oracle.CHKSUM_CRC32)
         else:
             want = oracle.encode(k, m, data, ct=oracle.CHKSUM_CRC32)
+        if legacy:
+            want = [oracle.legacy_headers(f) for f in want]
         for i in range(k + m):
             assert got[o, i, :80 + bs].tobytes() == want[i], f"obj {o} fragment {i}"
+    # the parity alone (no data fragments): same parity fragments
+    par = batch.stripe_buffer(n_obj, k, m, bs, device=gpu)
+    codec.encode(host.to(gpu), obj_len, parity=par[:, k:])
+    torch.cuda.synchronize()
+    assert np.array_equal(par[:, k:].cpu().numpy()[:, :, :80 + bs], got[:, k:, :80 + bs])
     full = (1 << (k + m)) - 1
     dest = [(o * 5 + 1) % (k + m) for o in range(n_obj)]
     rec = torch.zeros((n_obj, frags.shape[2]), dtype=torch.uint8, device=gpu)

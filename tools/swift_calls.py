@@ -88,11 +88,18 @@ def run(procs, size, op, seconds=2.0, k=10, m=4):
 
 
 def sweep(procs=(1, 4, 16), sizes=(1 << 20, 4 << 20), seconds=2.0):
+    """Every (size, op, P) run; a run whose workers fail is recorded with its
+    error (and stops the sweep: a worker's GPU fault is not retried)."""
     rows = []
     for size in sizes:
         for op in ("encode", "decode"):
             for p in procs:
-                rows.append(run(p, size, op, seconds))
+                try:
+                    rows.append(run(p, size, op, seconds))
+                except Exception as exc:  # noqa: BLE001 -- reported in the rows
+                    rows.append({"procs": p, "size": size, "op": op, "error": repr(exc),
+                                 "verified": False})
+                    return rows
     return rows
 
 
