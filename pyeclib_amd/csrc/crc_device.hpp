@@ -60,6 +60,25 @@ __device__ __forceinline__ uint32_t raw16(const uint4& x, uint32_t tab) {
   return a;
 }
 
+// raw16 without the per-dword fences: the 32 lookups of a piece may all be
+// in flight at once (for kernels with registers to spare -- the loader /
+// consumer encode -- where the fenced form's 4 dependent LDS round trips
+// per row and chunk left the CRC latency-bound).
+__device__ __forceinline__ uint32_t raw16_free(const uint4& x, uint32_t tab) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+  uint32_t a = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t lo = (w[d] << 2) & 0x3C3C3C3Cu, hi = (w[d] >> 2) & 0x3C3C3C3Cu;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t p = 8 * d + 2 * b;
+      a ^= lds32(tab + 64 * p + byte_of(lo, b)) ^ lds32(tab + 64 * (p + 1) + byte_of(hi, b));
+    }
+  }
+  return a;
+}
+
 // Dword d's share of raw16 (raw16(x) = XOR of raw_dword(x[d], d) over d):
 // 8 nibble lookups, for callers that spread a piece's CRC over time.
 __device__ __forceinline__ uint32_t raw_dword(uint32_t w, int d, uint32_t tab) {
@@ -96,9 +115,11 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t a) {
 }
 
 // Raw CRC of the wave's 1 KiB chunk, lane l holding bytes [16 l, 16 l + 16)
-// in v (CrcLaneTables at LDS byte `tab`): wave-uniform.
+// in v (CrcLaneTables at LDS byte `tab`): wave-uniform.  FREE: raw16_free.
+template <bool FREE = false>
 __device__ __forceinline__ uint32_t chunk_crc(const uint4& v, uint32_t tab, uint32_t lane4) {
-  return wave_xor(lane_map(raw16(v, tab), tab + offsetof(CrcLaneTables, lane), lane4));
+  const uint32_t r = FREE ? raw16_free(v, tab) : raw16(v, tab);
+  return wave_xor(lane_map(r, tab + offsetof(CrcLaneTables, lane), lane4));
 }
 
 // Set chksum[0] (header bytes 21..24) of the fragment header at `frag` to

@@ -1184,7 +1184,7 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
           buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x0 + (wave * SW + c) * 1024, x);
           if (crc)
             crc_store(p.crc_part_data + (static_cast<uint64_t>(o) * chunks + x0 / 1024 + wave * SW + c) * K + j,
-                      crcdev::chunk_crc(x, dma_ring_base<F, K>(), lane4));
+                      crcdev::chunk_crc<true>(x, dma_ring_base<F, K>(), lane4));
         }
       }
       ring = ring + 1 == R ? 0 : ring + 1;
@@ -1201,7 +1201,7 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
 #pragma unroll
         for (int q = 0; q < NR; ++q)
           if (static_cast<uint32_t>(q) < p.nrows)
-            crc_store(part + q, crcdev::chunk_crc(F::row(s[c], q), dma_ring_base<F, K>(), lane4));
+            crc_store(part + q, crcdev::chunk_crc<true>(F::row(s[c], q), dma_ring_base<F, K>(), lane4));
       }
       F::zero(s[c]);
     }

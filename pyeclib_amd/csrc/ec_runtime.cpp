@@ -257,6 +257,7 @@ struct RingSlot {
   uint8_t* host = nullptr;
   DevBuf dev;
   size_t cap = 0;
+  hipEvent_t cev = nullptr;  // the upload copy into `dev` done (on the upload stream)
   hipEvent_t ev = nullptr;
   bool pending = false;
 };
@@ -304,24 +305,35 @@ struct Instance {
   GfMatrix gen;
   std::mutex mu;
   hipStream_t stream = nullptr;
+  hipStream_t ustream = nullptr;  // descriptor uploads (ring_commit)
   // The end of this instance's work on every stream a launch of it has been
-  // queued on (a caller's few streams, the instance's own): when a call that
-  // launched on stream s returns, the event of s's entry is recorded on s
-  // (CallScope).  A device buffer the instance rewrites or frees is read
-  // only by launches on these streams, so waiting for these events -- on the
-  // GPU where the rewrite is itself queued, on the host where it is not --
-  // replaces a device-wide synchronisation: other instances' and other
-  // threads' work is never waited for, and every error is returned.  A
-  // stream handle is used only during a call on it, so a caller may destroy
-  // its stream once the call returns; entries whose work has completed are
-  // dropped, so a caller taking a new stream per call does not grow the list.
+  // queued on (a caller's streams, the instance's own), so that a device
+  // buffer the instance rewrites or frees -- read only by launches on these
+  // streams -- is rewritten after them: GPU-side where the rewrite is itself
+  // queued, on the host where it is not.  That replaces a device-wide
+  // synchronisation: other instances' and threads' work is not waited for,
+  // and every error is returned.
+  //   * A caller's stream handle is used only during a call on it (a caller
+  //     may destroy its stream once the call returns).  While the instance
+  //     has seen ONE caller stream, nothing is recorded: its work is ordered
+  //     by the stream itself, and an end mark per call cost the bench's
+  //     encode 2.4 % (6.5 us of 274; profiles/r05b_ab_endmark.txt).  When a
+  //     second caller stream appears, the first one's calls are finished
+  //     once with a device synchronise (its handle may be gone), and from
+  //     then on every call records its end mark on its stream (CallScope).
+  //   * The instance's own streams are valid while it lives: marked lazily,
+  //     when something must wait for them.
+  // Entries whose recorded work has completed are dropped, so a caller
+  // taking a new stream per call does not grow the list.
   struct StreamMark {
     hipStream_t s;
     hipEvent_t ev;
-    bool open;      // launched on during the current call: record at its end
+    bool own;       // the instance's own stream
+    bool open;      // launched on during the current call
     bool recorded;  // ev marks the end of this instance's work on s
   };
   std::vector<StreamMark> marks;
+  bool multi = false;  // has seen two caller streams: caller calls are marked
   DevBuf enc_tables;  // passes x k x 64 u64
   // GF(2^16) with 4 < m <= 8: one eight-row table set (k x 1 KiB), so encode
   // reads the object once (ec_kernels_impl.hpp Gf16x8); the four-row passes
@@ -375,6 +387,35 @@ struct Instance {
   // bytes of one table set (k inputs x up to 4 rows)
   size_t table_bytes() const { return static_cast<size_t>(k) * table_bytes_per_input(code.w); }
 
+  bool is_own(hipStream_t s) const {
+    if (s == stream) return true;
+    for (hipStream_t h : hstream)
+      if (h && s == h) return true;
+    return false;
+  }
+  // Finish the unmarked work of every caller stream but s (all of them
+  // when !keep; single-stream mode: their handles may be gone) and forget them.
+  hipError_t drop_unmarked_callers(hipStream_t s, bool keep = true) {
+    auto gone = [&](const StreamMark& k) {
+      return !k.own && !k.open && !k.recorded && !(keep && k.s == s);
+    };
+    bool any = false;
+    for (auto& k : marks) any |= gone(k);
+    if (!any) return hipSuccess;
+    const hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return e;
+    size_t j = 0;
+    for (size_t i = 0; i < marks.size(); ++i) {
+      StreamMark& k = marks[i];
+      if (gone(k)) {
+        (void)hipEventDestroy(k.ev);
+        continue;
+      }
+      marks[j++] = k;
+    }
+    marks.resize(j);
+    return hipSuccess;
+  }
   // A launch of this instance is about to be queued on s (during a call).
   hipError_t note_stream(hipStream_t s) {
     for (auto& k : marks)
@@ -382,31 +423,47 @@ struct Instance {
         k.open = true;
         return hipSuccess;
       }
+    const bool own = is_own(s);
+    if (!own && !multi) {
+      bool other = false;
+      for (auto& k : marks) other |= !k.own;
+      if (other) {  // a second caller stream
+        const hipError_t e = drop_unmarked_callers(s);
+        if (e != hipSuccess) return e;
+        multi = true;
+      }
+    }
     hipEvent_t ev = nullptr;
     const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e != hipSuccess) return e;
-    marks.push_back({s, ev, true, false});
+    marks.push_back({s, ev, own, true, false});
     return hipSuccess;
   }
-  // End of a call: mark the end of its work on every stream it launched on
-  // (those handles are the call's own, valid now).
+  // End of a call: mark the end of its work on every caller stream it
+  // launched on (those handles are the call's own, valid now) once the
+  // instance has seen two caller streams.
   hipError_t end_call() {
     hipError_t first = hipSuccess;
     for (auto& k : marks) {
       if (!k.open) continue;
       k.open = false;
+      if (k.own) continue;  // marked when something waits for it
+      if (!multi) {
+        k.recorded = false;  // single caller stream: unmarked
+        continue;
+      }
       const hipError_t e = hipEventRecord(k.ev, k.s);
       k.recorded = e == hipSuccess;
       if (e != hipSuccess && first == hipSuccess) first = e;
     }
     return first;
   }
-  // Drop the entries (other than s's) whose recorded work has completed.
+  // Drop the caller entries (other than s's) whose recorded work has completed.
   void prune_marks(hipStream_t s) {
     size_t j = 0;
     for (size_t i = 0; i < marks.size(); ++i) {
       StreamMark& k = marks[i];
-      if (k.s != s && !k.open && k.recorded && hipEventQuery(k.ev) == hipSuccess) {
+      if (k.s != s && !k.own && !k.open && k.recorded && hipEventQuery(k.ev) == hipSuccess) {
         (void)hipEventDestroy(k.ev);
         continue;
       }
@@ -416,29 +473,33 @@ struct Instance {
   }
   // GPU-side: work queued on s from now on runs after everything this
   // instance queued so far on its other streams (s's own work is ordered
-  // already): earlier calls' through their end marks, the current call's
-  // (a host pipeline deals chunks over several streams) through a mark
-  // recorded now.
+  // already): the current call's other streams and the instance's own
+  // through a mark recorded now, earlier calls' caller streams through their
+  // end marks -- or, unmarked, by a device synchronise.
   hipError_t order_after_streams(hipStream_t s) {
     prune_marks(s);
+    hipError_t e = drop_unmarked_callers(s);
+    if (e != hipSuccess) return e;
     for (auto& k : marks) {
       if (k.s == s) continue;
-      if (k.open) {
-        const hipError_t e = hipEventRecord(k.ev, k.s);
-        if (e != hipSuccess) return e;
+      if (k.open || k.own) {
+        if ((e = hipEventRecord(k.ev, k.s)) != hipSuccess) return e;
         k.recorded = true;
       }
       if (!k.recorded) continue;
-      const hipError_t e = hipStreamWaitEvent(s, k.ev, 0);
-      if (e != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(s, k.ev, 0)) != hipSuccess) return e;
     }
     return hipSuccess;
   }
-  // Host-side: wait for everything queued so far on the instance's streams
-  // (the current call's launches first get their end marks).
+  // Host-side: wait for everything queued so far on the instance's streams.
   hipError_t wait_streams() {
-    hipError_t first = end_call();
+    hipError_t first = drop_unmarked_callers(nullptr, false);
     for (auto& k : marks) {
+      if (k.open || k.own) {
+        const hipError_t e = hipEventRecord(k.ev, k.s);
+        if (e != hipSuccess && first == hipSuccess) first = e;
+        k.recorded = e == hipSuccess;
+      }
       if (!k.recorded) continue;
       const hipError_t e = hipEventSynchronize(k.ev);
       if (e != hipSuccess && first == hipSuccess) first = e;
@@ -466,11 +527,13 @@ struct Instance {
     dec_cache.release();
     rec_cache.release();
     hdr_cache.release();
+    if (ustream) (void)hipStreamSynchronize(ustream);
     for (auto& r : ring) {
       if (r.ev) {
         (void)hipEventSynchronize(r.ev);
         (void)hipEventDestroy(r.ev);
       }
+      if (r.cev) (void)hipEventDestroy(r.cev);
       if (r.host) (void)hipHostFree(r.host);
       r.dev.release();
     }
@@ -484,6 +547,7 @@ struct Instance {
     for (auto& kv : crc_finish) kv.second.release();
     for (auto& c : crc_part) c.buf.release();
     if (stream) (void)hipStreamDestroy(stream);
+    if (ustream) (void)hipStreamDestroy(ustream);
   }
 
   // Acquire a ring slot with at least n bytes; waits for its previous use.
@@ -510,8 +574,24 @@ struct Instance {
     }
     return &r;
   }
+  // Copy a slot's n bytes for a launch on s.  The copy runs on the
+  // instance's upload stream, beside the kernels s is still running, and s
+  // waits for it: a call with new descriptors then adds no copy between two
+  // kernels on s (decode with erasure masks new every call, pyeclib_c.c:878;
+  // the copy on s itself had cost that decode ~12 % over the cached-descriptor
+  // call, BENCH_r04 decode_fresh_ms).  The slot's buffers are rewritten only
+  // after ring_acquire's wait for the launch that read them, which ran after
+  // this copy.
   hipError_t ring_commit(RingSlot* r, size_t n, hipStream_t s) {
-    return hipMemcpyAsync(r->dev.p, r->host, n, hipMemcpyHostToDevice, s);
+    hipError_t e = hipSuccess;
+    if (!ustream && (e = hipStreamCreateWithFlags(&ustream, hipStreamNonBlocking)) != hipSuccess)
+      return e;
+    if (!r->cev && (e = hipEventCreateWithFlags(&r->cev, hipEventDisableTiming)) != hipSuccess)
+      return e;
+    if ((e = hipMemcpyAsync(r->dev.p, r->host, n, hipMemcpyHostToDevice, ustream)) != hipSuccess)
+      return e;
+    if ((e = hipEventRecord(r->cev, ustream)) != hipSuccess) return e;
+    return hipStreamWaitEvent(s, r->cev, 0);
   }
   hipError_t ring_release(RingSlot* r, hipStream_t s) {
     hipError_t e = hipEventRecord(r->ev, s);
@@ -522,19 +602,12 @@ struct Instance {
 
 // Held by every entry point that may launch (after the instance lock): the
 // call's end marks are recorded however it returns (Instance::end_call).
-// (A/B builds: ECAMD_NO_END_MARK=1 skips them -- single-stream timing only.)
 struct CallScope {
   Instance& I;
   explicit CallScope(Instance& i) : I(i) {}
   CallScope(const CallScope&) = delete;
   CallScope& operator=(const CallScope&) = delete;
-  ~CallScope() {
-    if (kAB && ab_knob("ECAMD_NO_END_MARK", 0)) {
-      for (auto& k : I.marks) k.open = false;
-      return;
-    }
-    (void)I.end_call();
-  }
+  ~CallScope() { (void)I.end_call(); }
 };
 
 // Where one launch's small table came from (see UploadCache).

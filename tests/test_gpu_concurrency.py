@@ -172,3 +172,44 @@ def test_staged_pipeline_reuses_patterns_across_streams(gpu, oracle, monkeypatch
             codec.reconstruct_host(hfr, n, masks, dest, rec)
             for o in range(B):
                 assert rec[o, :fl].numpy().tobytes() == frags[o][dest[o]], (rep, o)
+
+
+def test_destroyed_caller_streams(gpu, oracle, monkeypatch):
+    """A caller may destroy its stream once a call on it has returned (round-4
+    advice): calls on a stream created and destroyed per call, on one
+    instance with a 5-slot table pool -- so later calls recycle the pool
+    (and rewrite cached descriptors) after launches queued on streams that
+    no longer exist -- never touch those handles, and every output is right."""
+    import ctypes
+    import torch
+    from pyeclib_amd import batch
+    monkeypatch.setenv("ECAMD_POOL_SLOTS", "5")
+    import importlib.util
+    lib = os.path.join(importlib.util.find_spec("torch").submodule_search_locations[0], "lib",
+                       "libamdhip64.so")
+    hip = ctypes.CDLL(lib if os.path.exists(lib) else "libamdhip64.so")  # the loaded runtime
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    k, m, n, B = 10, 4, (64 << 10) + 10, 12
+    codec = batch.BatchCodec(k, m)
+    host = _objects(B, n, 7)
+    objs = torch.from_numpy(host).to(gpu)
+    stripes = batch.stripe_buffer(B, k, m, codec.blocksize(n), device=gpu)
+    codec.encode(objs, n, parity=stripes[:, k:], data=stripes[:, :k])
+    torch.cuda.synchronize()
+    rng = random.Random(11)
+    full = (1 << (k + m)) - 1
+    for call in range(40):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        masks = [full & ~sum(1 << i for i in rng.sample(range(k + m), m)) for _ in range(B)]
+        if call % 3 == 0:  # the same masks twice in a row: the cached descriptor path
+            masks = prev if call else masks
+        prev = masks
+        out = torch.zeros_like(objs)
+        torch.cuda.synchronize()
+        codec.decode(stripes, n, masks, out, stream=s.value)
+        assert hip.hipStreamSynchronize(s) == 0
+        assert hip.hipStreamDestroy(s) == 0
+        assert torch.equal(out[:, :n].cpu(), torch.from_numpy(host[:, :n])), call
