@@ -1154,6 +1154,27 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   typename F::Acc s[SW];
 #pragma unroll
   for (int c = 0; c < SW; ++c) F::zero(s[c]);
+  // inline_crc32 (SW = 1): an item's parity chunk CRCs are taken during the
+  // NEXT item's K slots, kCrcSteps / K steps of 8 lookups per slot (row q:
+  // its raw16 by dword, then its lane map, the wave XOR and the store), so
+  // no wave carries a burst of lookups into a ring barrier -- taken all at
+  // the item's end they held the ring for ~3.8 K LDS cycles per CU and item
+  // (the CRC encode ran 1.28x the plain one; profiles/r05b_*).
+  constexpr int kCrcSteps = 5 * NR;
+  uint4 crow[NR];
+  uint32_t cacc[NR];
+  uint32_t* cpart = p.crc_part;
+  bool cpend = false;
+  auto crc_step = [&](int u) {
+    const int q = u / 5, d = u % 5;
+    if (d < 4) {
+      const uint32_t w = d == 0 ? crow[q].x : d == 1 ? crow[q].y : d == 2 ? crow[q].z : crow[q].w;
+      cacc[q] ^= crcdev::raw_dword(w, d, dma_ring_base<F, K>());
+    } else if (static_cast<uint32_t>(q) < p.nrows) {
+      crc_store(cpart + q, crcdev::wave_xor(crcdev::lane_map(
+                               cacc[q], dma_ring_base<F, K>() + offsetof(CrcLaneTables, lane), lane4)));
+    }
+  };
 #pragma clang loop unroll(disable)
   for (uint32_t i = 0; i < n_items; ++i) {
     uint32_t o, x0;
@@ -1184,7 +1205,13 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
           buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x0 + (wave * SW + c) * 1024, x);
           if (crc)
             crc_store(p.crc_part_data + (static_cast<uint64_t>(o) * chunks + x0 / 1024 + wave * SW + c) * K + j,
-                      crcdev::chunk_crc<true>(x, dma_ring_base<F, K>(), lane4));
+                      crcdev::chunk_crc(x, dma_ring_base<F, K>(), lane4));
+        }
+      }
+      if constexpr (SW == 1) {
+        if (cpend) {  // the previous item's CRC steps [kCrcSteps j / K, kCrcSteps (j + 1) / K)
+#pragma unroll
+          for (int u = j * kCrcSteps / K; u < (j + 1) * kCrcSteps / K; ++u) crc_step(u);
         }
       }
       ring = ring + 1 == R ? 0 : ring + 1;
@@ -1198,12 +1225,28 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
         buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, F::row(s[c], q));
       if (crc) {
         uint32_t* part = p.crc_part + (static_cast<uint64_t>(o) * chunks + x0 / 1024 + wave * SW + c) * p.m + p.row0;
+        if constexpr (SW == 1) {  // taken during the next item (or after the last)
 #pragma unroll
-        for (int q = 0; q < NR; ++q)
-          if (static_cast<uint32_t>(q) < p.nrows)
-            crc_store(part + q, crcdev::chunk_crc<true>(F::row(s[c], q), dma_ring_base<F, K>(), lane4));
+          for (int q = 0; q < NR; ++q) {
+            crow[q] = F::row(s[c], q);
+            cacc[q] = 0;
+          }
+          cpart = part;
+          cpend = true;
+        } else {
+#pragma unroll
+          for (int q = 0; q < NR; ++q)
+            if (static_cast<uint32_t>(q) < p.nrows)
+              crc_store(part + q, crcdev::chunk_crc(F::row(s[c], q), dma_ring_base<F, K>(), lane4));
+        }
       }
       F::zero(s[c]);
+    }
+  }
+  if constexpr (SW == 1) {
+    if (cpend) {  // the block's last item
+#pragma unroll
+      for (int u = 0; u < kCrcSteps; ++u) crc_step(u);
     }
   }
   if (loader) wait_vm<0>();  // no DMA may land in LDS after the block ends

@@ -58,6 +58,23 @@ def main():
         print(f"{label:7s} host call median {np.median(host_us[2:]):8.1f} us  "
               f"event span median {np.median(span_us[2:]):8.1f} us  (first {host_us[0]:.0f} / {span_us[0]:.0f})")
         assert torch.equal(out, objs)
+    # back to back (bench.py decode_fresh_ms's shape): 16 calls with no
+    # synchronisation between them, masks new every call vs repeated
+    for label, gen in (("steady-fresh", lambda i: masks(300 + i)), ("steady-repeat", lambda i: masks(7))):
+        mks = [gen(i) for i in range(16)]
+        for rep in range(2):  # the first pass brings any new patterns into the pool
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record()
+            for mk in mks:
+                codec.decode(stripes, n, mk, out)
+            t1 = time.perf_counter()
+            e1.record()
+            torch.cuda.synchronize()
+        print(f"{label:13s} per call: host {(t1 - t0) * 1e6 / len(mks):8.1f} us  "
+              f"event span {e0.elapsed_time(e1) * 1e3 / len(mks):8.1f} us")
+        assert torch.equal(out, objs)
 
 
 if __name__ == "__main__":
