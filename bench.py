@@ -801,6 +801,11 @@ def main():
         if default_workload else {}
     lib_id = _native.build_id()
     pmc_ok = pmc.get("library_id") == lib_id
+    # rocprof per-dispatch kernel times of this same library (profiles/
+    # kernel_stats.json, tools/kernel_stats_summary.py), beside the events
+    kst = (load_pmc(os.path.join(ROOT, "profiles", "kernel_stats.json")) or {}) \
+        if default_workload else {}
+    kst_ok = kst.get("library_id") == lib_id
     traffic = pmc.get(dom, {}).get("hbm_bytes_per_launch") if pmc_ok else None
     achieved = kernels[dom]["GBps"]
 
@@ -818,6 +823,18 @@ def main():
                 "traffic_by_kernel": ({kk: pmc.get(kk, {}).get("hbm_bytes_per_launch")
                                        for kk in kernels} if pmc_ok else None),
                 "library_id": lib_id}
+    if kst_ok and dom in kst:
+        # the same algorithmic bytes over rocprof's kernel time: every
+        # dispatch of the profiled run (rocprofv3 --stats) and its timed steps
+        def frac_us(us, kk):
+            return round(kernels[kk]["bytes"] / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+        roofline["frac_rocprof"] = frac_us(kst[dom]["avg_us"], dom)
+        roofline["frac_rocprof_timed"] = frac_us(kst[dom]["timed_avg_us"], dom)
+        roofline["rocprof_us"] = {kk: {"avg": kst[kk]["avg_us"], "timed_avg": kst[kk]["timed_avg_us"],
+                                       "frac": frac_us(kst[kk]["avg_us"], kk),
+                                       "frac_timed": frac_us(kst[kk]["timed_avg_us"], kk)}
+                                  for kk in kernels if kk in kst}
+        roofline["rocprof_source"] = "profiles/kernel_stats.json (tools/kernel_stats_summary.py)"
 
     metric = METRIC if default_workload else (
         f"device-resident encode+{two} GiB/s, {args.ec_type} k={k} m={m}, {n} B objects"

@@ -81,12 +81,15 @@ for s in $STEPS; do
     (cd $R && timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err)
     cat $O/bench.json ;;
   prof)
-    (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run \
-      -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-verify --no-host > $O/prof_bench.json 2> $O/prof.err)
+    # per-dispatch kernel trace of the bench's headline steps (no extra legs,
+    # so the last 20 dispatches of each kernel are the timed steps), summarised
+    # into kernel_stats.json for bench.py's roofline (frac_rocprof)
+    (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run \
+      -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-verify --no-host \
+      --fresh-steps 0 --full-stripe-steps 0 > $O/prof_bench.json 2> $O/prof.err)
     cat $O/prof_bench.json
-    find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \;
-    [ -f $O/kernel_stats.csv ] || python3 $R/tools/rocpd_stats.py $O/prof $O/kernel_stats.csv > $O/kernel_stats.txt
-    head -12 $O/kernel_stats.txt 2>/dev/null || true ;;
+    python3 $R/tools/kernel_stats_summary.py $O/prof $O/kernel_stats.json --steps 20
+    find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \; ;;
   pmc)
     (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run \
       -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host > $O/pmc_fetch.log 2>&1)
