@@ -2198,46 +2198,56 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
                                 stream, per_cu, true);
     }
   }
-  if (p.crc_lanes != nullptr) {
-    if constexpr (F::kRows > kRowsPerPass) {
-      return hipErrorInvalidValue;  // the inline CRC runs in four-row passes
-    } else {
-      uint32_t chunks = 0;
-      hipError_t e = hipSuccess;
-      bool dma = false;
-      if constexpr (K >= kDmaMinK) {
-        dma = dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) && !ab_knob("ECAMD_CRC_STREAM", 0);
-        if (dma)
-          e = data ? launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream, &chunks)
-                   : launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream, &chunks);
-      }
-      if (!dma) {
-        p.fused_edges = 1;
-        chunks = crc_chunks(p.tiles, p.tile_ch);
-        const size_t crc_lds = crc_lds_base<F, K>() + kCrcLaneBytes;
-        e = data ? launch_edges_apart(encode_kernel<F, K, NR, false, true, 1, false, 0, false, true>, p,
-                                      crc_lds, p.n_obj * p.tiles, edge_items, stream, kEncodePerCu, true)
-                 : launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, false, 0, false, true>, p,
-                                      crc_lds, p.n_obj * p.tiles, edge_items, stream, kEncodePerCu, true);
-      }
-      if (e != hipSuccess) return e;
-      return encode_crc_finish<K>(p, data, chunks, stream);
+  // Which kernel.  For k >= kDmaMinK the loader / consumer encode takes
+  // every launch with the full stripe or the inline CRC, whatever the batch
+  // size -- the stream kernel exists in those forms only for k < kDmaMinK
+  // (round 5: the library held every (field, k, rows, data, CRC) stream
+  // form, 149 MB; those forms only matter for throughput on large batches,
+  // where the loader / consumer kernel is the faster one anyway) -- and the
+  // plain parity encode of a batch with a 16 KiB item per CU.  Its input
+  // offsets j * bs + x are 32-bit.
+  const bool crc = p.crc_lanes != nullptr;
+  uint32_t chunks = 0;
+  hipError_t e = hipErrorInvalidValue;
+  bool done = false;
+  if constexpr (F::kRows <= kRowsPerPass && K >= kDmaMinK) {
+    if (crc || data || (dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) &&
+                        !ab_knob("ECAMD_ENC_STREAM", 0))) {
+      if (static_cast<uint64_t>(K) * p.bs + 65536u > 0xFFFFFFFFull) return hipErrorInvalidValue;
+      e = data ? launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream, &chunks)
+               : launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream, &chunks);
+      done = true;
     }
   }
-  // the loader / consumer encode (encode_dma_kernel) for k >= kDmaMinK; its
-  // input offsets j * bs + x are 32-bit
-  if constexpr (F::kRows <= kRowsPerPass && K >= kDmaMinK) {
-    if (dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) && !ab_knob("ECAMD_ENC_STREAM", 0))
-      return data ? launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream)
-                  : launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream);
+  if (!done) {
+    p.fused_edges = 1;
+    const uint32_t items = p.n_obj * p.tiles;
+    chunks = crc_chunks(p.tiles, p.tile_ch);
+    if constexpr (F::kRows > kRowsPerPass) {
+      if (crc) return hipErrorInvalidValue;  // the inline CRC runs in four-row passes
+      e = data ? launch_edges_apart(encode_kernel<F, K, NR, false, true>, p, lds, items, edge_items,
+                                    stream, kEncodePerCu, true)
+               : launch_edges_apart(encode_kernel<F, K, NR>, p, lds, items, edge_items, stream,
+                                    kEncodePerCu, true);
+    } else if constexpr (K < kDmaMinK) {
+      const size_t crc_lds = crc_lds_base<F, K>() + kCrcLaneBytes;
+      if (crc)
+        e = data ? launch_edges_apart(encode_kernel<F, K, NR, false, true, 1, false, 0, false, true>, p,
+                                      crc_lds, items, edge_items, stream, kEncodePerCu, true)
+                 : launch_edges_apart(encode_kernel<F, K, NR, false, false, 1, false, 0, false, true>, p,
+                                      crc_lds, items, edge_items, stream, kEncodePerCu, true);
+      else
+        e = data ? launch_edges_apart(encode_kernel<F, K, NR, false, true>, p, lds, items, edge_items,
+                                      stream, kEncodePerCu, true)
+                 : launch_edges_apart(encode_kernel<F, K, NR>, p, lds, items, edge_items, stream,
+                                      kEncodePerCu, true);
+    } else {
+      e = launch_edges_apart(encode_kernel<F, K, NR>, p, lds, items, edge_items, stream,
+                             kEncodePerCu, true);
+    }
   }
-  p.fused_edges = 1;
-  const uint32_t items = p.n_obj * p.tiles;
-  if (data)
-    return launch_edges_apart(encode_kernel<F, K, NR, false, true>, p, lds, items, edge_items,
-                              stream, kEncodePerCu, true);
-  return launch_edges_apart(encode_kernel<F, K, NR>, p, lds, items, edge_items, stream,
-                            kEncodePerCu, true);
+  if (e != hipSuccess || !crc) return e;
+  return encode_crc_finish<K>(p, data, chunks, stream);
 }
 
 // LDS of a decode launch: two table slots.

@@ -1330,6 +1330,11 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
   // inline_crc32: every launch stores its chunks' CRC partials, and the
   // launcher runs the finishing pass (parity rows; data fragments too)
   const bool crc = headers && I.ct == CHKSUM_CRC32 && bs > 0;
+  // those forms (and the full stripe) run the loader / consumer kernel for
+  // k >= 4, whose input offsets j * bs + x are 32-bit (ec_kernels_impl.hpp
+  // launch_encode_k)
+  if ((crc || data) && k >= kDmaMinK && static_cast<uint64_t>(k) * bs + 65536u > 0xFFFFFFFFull)
+    return -EINVALIDPARAMS;
   const void* crc_lanes = nullptr;
   const void* crc_fin = nullptr;
   uint32_t* crc_part = nullptr;
