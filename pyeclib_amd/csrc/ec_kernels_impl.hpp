@@ -1068,8 +1068,12 @@ __host__ __device__ constexpr uint32_t dma_lds_bytes(bool crc = false) {
 // COMB (A/B): groups of COMB consecutive blocks share an object, block r of a
 // group taking its tiles r, r + COMB, ... (the order a Horner CRC with a
 // COMB-item stride could use); G / COMB objects in flight.
+// CV (A/B, inline CRC): 0 = the parity chunks' CRC steps deferred over the
+// next item's slots (the product), 1 = taken at the item's end, 2 = at the
+// item's end with unfenced raw16 lookups (crcdev::raw16_free).
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
-          bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0, int COMB = 0>
+          bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0, int COMB = 0,
+          int CV = 0>
 __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   static_assert(R >= 2 && R <= K + 1, "ring of 2 .. K + 1 slots");
   static_assert(L == 2 || L == 4 || L == 8 || L == 16, "loader waves");
@@ -1208,7 +1212,7 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
                       crcdev::chunk_crc(x, dma_ring_base<F, K>(), lane4));
         }
       }
-      if constexpr (SW == 1) {
+      if constexpr (SW == 1 && CV == 0) {
         if (cpend) {  // the previous item's CRC steps [kCrcSteps j / K, kCrcSteps (j + 1) / K)
 #pragma unroll
           for (int u = j * kCrcSteps / K; u < (j + 1) * kCrcSteps / K; ++u) crc_step(u);
@@ -1225,7 +1229,7 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
         buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, F::row(s[c], q));
       if (crc) {
         uint32_t* part = p.crc_part + (static_cast<uint64_t>(o) * chunks + x0 / 1024 + wave * SW + c) * p.m + p.row0;
-        if constexpr (SW == 1) {  // taken during the next item (or after the last)
+        if constexpr (SW == 1 && CV == 0) {  // taken during the next item (or after the last)
 #pragma unroll
           for (int q = 0; q < NR; ++q) {
             crow[q] = F::row(s[c], q);
@@ -1237,13 +1241,13 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
 #pragma unroll
           for (int q = 0; q < NR; ++q)
             if (static_cast<uint32_t>(q) < p.nrows)
-              crc_store(part + q, crcdev::chunk_crc(F::row(s[c], q), dma_ring_base<F, K>(), lane4));
+              crc_store(part + q, crcdev::chunk_crc<CV == 2>(F::row(s[c], q), dma_ring_base<F, K>(), lane4));
         }
       }
       F::zero(s[c]);
     }
   }
-  if constexpr (SW == 1) {
+  if constexpr (SW == 1 && CV == 0) {
     if (cpend) {  // the block's last item
 #pragma unroll
       for (int u = 0; u < kCrcSteps; ++u) crc_step(u);
@@ -1442,7 +1446,8 @@ __device__ __forceinline__ Rsrc rsrc_out(const void* base) {
 // Stores that do not apply (parity inputs, rows past n_out) go to voffset
 // kDrop and are discarded by the range check, so every item issues the same
 // memory instructions.  NOCOMP: memory-only probe (no lookups; wrong rows).
-template <class F, int K, int MODE, bool NOCOMP = false, int NBX = 0, bool SDESC = true>
+template <class F, int K, int MODE, bool NOCOMP = false, int NBX = 0, bool SDESC = true,
+          bool CRCFREE = false>
 __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st,
                                                 TablePre<F, K>& pre) {
   constexpr int NB = NBX ? NBX : stream_bufs<K>();  // NBX: A/B (divides K)
@@ -1536,7 +1541,7 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
       buf_st(out, lane16, kHeaderBytes + x, F::row(s, 0));
       if (p.crc_part != nullptr)  // inline_crc32: the chunk's raw CRC (launch_decode_mode)
         crc_store(p.crc_part + static_cast<uint64_t>(o) * crc_chunks(p.tiles, p.tile_ch) + x / kChunkBytes,
-                  crcdev::chunk_crc(F::row(s, 0), 2 * table_slot_bytes(K, F::kW), lane_id() * 4));
+                  crcdev::chunk_crc<CRCFREE>(F::row(s, 0), 2 * table_slot_bytes(K, F::kW), lane_id() * 4));
     } else {
       const uint32_t e = d.n_out();
 #pragma unroll
@@ -1626,7 +1631,9 @@ __device__ __forceinline__ void decode_edges(const DecodeParams& p, uint32_t fir
 // counted from the end of the grid (see encode_kernel), then the interior
 // stream.  The interior's first table change goes into the LDS slot the edge
 // items did not use, behind a barrier, as between any two items.
-template <class F, int K, int MODE, bool NOCOMP = false, int NBX = 0, bool SDESC = true>
+// CRCFREE (A/B): reconstruct's chunk CRC with unfenced raw16 lookups.
+template <class F, int K, int MODE, bool NOCOMP = false, int NBX = 0, bool SDESC = true,
+          bool CRCFREE = false>
 __global__ void __launch_bounds__(kThreadsPerBlock)
     __attribute__((amdgpu_waves_per_eu(NBX > 6 ? 4 : kDecodeOcc, 8))) decode_kernel(DecodeParams p) {
   Slots st{0xFFFFFFFFu, 1u};
@@ -1645,7 +1652,7 @@ __global__ void __launch_bounds__(kThreadsPerBlock)
       return;
     }
   }
-  decode_interior<F, K, MODE, NOCOMP, NBX, SDESC>(p, st, pre);
+  decode_interior<F, K, MODE, NOCOMP, NBX, SDESC, CRCFREE>(p, st, pre);
 }
 
 // The edge work in a launch of its own (side-stream variant, ECAMD_EDGE_SIDE=1).
@@ -2072,11 +2079,12 @@ hipError_t encode_crc_finish(const EncodeParams& p, bool data, uint32_t chunks, 
 // k >= kDmaMinK when the batch has a 16 KiB item for every CU (smaller
 // batches keep the stream kernel's 4 KiB items).
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
-          bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0, int COMB = 0>
+          bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0, int COMB = 0,
+          int CV = 0>
 hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream, uint32_t* chunks = nullptr) {
   set_tiles(p, last_room(p.bs, p.obj_len, K), 1024u * W * SW / kTile);
   if (chunks) *chunks = crc_chunks(p.tiles, p.tile_ch);
-  const auto kern = encode_dma_kernel<F, K, NR, R, NT, L, SW, W, DATA, NOCOMP, CONTIG, RUNS, COMB>;
+  const auto kern = encode_dma_kernel<F, K, NR, R, NT, L, SW, W, DATA, NOCOMP, CONTIG, RUNS, COMB, CV>;
   const size_t lds = dma_lds_bytes<F, K, R, SW, W>(p.crc_lanes != nullptr);
   if (!lds_starts_at_zero(reinterpret_cast<const void*>(kern))) return hipErrorInvalidKernelFile;
   const int cus = device_cus();
@@ -2210,6 +2218,19 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   uint32_t chunks = 0;
   hipError_t e = hipErrorInvalidValue;
   bool done = false;
+  if constexpr (kAB && K == 10 && NR == 4) {
+    // A/B: the inline CRC's forms (CV, see encode_dma_kernel) and a 4-slot ring
+    const int cv = ab_knob("ECAMD_CRC_V", 0), cr = ab_knob("ECAMD_CRC_R", 3);
+    if (crc && !data && (cv != 0 || cr != 3)) {
+      if (cv == 1 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 1>(p, stream, &chunks);
+      else if (cv == 2 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 2>(p, stream, &chunks);
+      else if (cv == 0 && cr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 12>(p, stream, &chunks);
+      else if (cv == 1 && cr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 12, false, false, false, 0, 0, 1>(p, stream, &chunks);
+      else return hipErrorInvalidValue;
+      if (e != hipSuccess) return e;
+      return encode_crc_finish<K>(p, data, chunks, stream);
+    }
+  }
   if constexpr (F::kRows <= kRowsPerPass && K >= kDmaMinK) {
     if (crc || data || (dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) &&
                         !ab_knob("ECAMD_ENC_STREAM", 0))) {
@@ -2357,9 +2378,11 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
     if (MODE != kReconstruct && p.crc_lanes != nullptr) return hipErrorInvalidValue;
     if (crc) {
       p.fused_edges = 1;
-      hipError_t e = launch_edges_apart(decode_kernel<F, K, MODE>, p, lds + kCrcLaneBytes,
-                                        p.n_obj * p.tiles, edge_items, stream, kReconstructPerCu,
-                                        kDecodeXcd);
+      auto kern = decode_kernel<F, K, MODE>;
+      if constexpr (kAB && K == 10 && MODE == kReconstruct)
+        if (ab_knob("ECAMD_REC_CRC_FREE", 0)) kern = decode_kernel<F, K, MODE, false, 0, true, true>;
+      hipError_t e = launch_edges_apart(kern, p, lds + kCrcLaneBytes, p.n_obj * p.tiles, edge_items,
+                                        stream, kReconstructPerCu, kDecodeXcd);
       if (e != hipSuccess) return e;
       return crc_finish(p.out, 0, p.out_stride, p.crc_part, 1, 0, p.crc_lanes, p.crc_finish_tables,
                         p.n_obj, 1, p.bs, crc_chunks(p.tiles, p.tile_ch), stream);

@@ -65,7 +65,7 @@ def test_product_library_has_no_ab_switches():
                  "ECAMD_ENC_NB", "ECAMD_DEC_NB", "ECAMD_EDGE_SIDE", "ECAMD_DATA_COPY",
                  "ECAMD_ENC_PER_CU", "ECAMD_DEC_PER_CU", "ECAMD_REC_PER_CU",
                  "ECAMD_CRC_PER_CU", "ECAMD_CRC_NTL", "ECAMD_XCD", "ECAMD_ENC_R3",
-                 "ECAMD_DEC_R3", "ECAMD_CRC_STREAM", "ECAMD_NO_END_MARK"):
+                 "ECAMD_DEC_R3", "ECAMD_CRC_STREAM", "ECAMD_CRC_V", "ECAMD_CRC_R", "ECAMD_REC_CRC_FREE"):
         assert name not in text, f"{name} is in the product library"
     exported = set(re.findall(r"\bT (\w+)", _nm("-D", "--defined-only", LIB)))
     assert "ecamd_ab_set" not in exported
