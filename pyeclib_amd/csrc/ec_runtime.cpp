@@ -344,20 +344,18 @@ struct Instance {
   uint32_t pool_slots = 0, pool_used = 0;
   uint64_t pool_gen = 1;  // bumped whenever slots are recycled
   // recorded where the pool was last recycled, after the waits for every
-  // launch that could read the old table sets: a table copy queued on
-  // another stream waits for it before overwriting a slot
+  // launch that could read the old table sets: the table copies (upload
+  // stream) wait for it before overwriting a slot
   hipEvent_t pool_gen_ev = nullptr;
-  hipStream_t pool_gen_stream = nullptr;
   bool pool_gen_pending = false;
   std::unordered_map<uint64_t, uint32_t> pool_index;
   // table sets of patterns new in this call: built on the host into
   // pool_stage (slots pool_stage_first..), uploaded by pool_commit with ONE
-  // async copy on the call's stream ahead of its launch; pool_ev marks the
-  // last such copy for launches on other streams
+  // async copy on the upload stream ahead of its launch; pool_ev marks the
+  // last such copy, which every launch that reads the pool waits for
   std::vector<uint8_t> pool_stage;
   uint32_t pool_stage_first = 0;
-  hipEvent_t pool_ev = nullptr;
-  hipStream_t pool_ev_stream = nullptr;
+  hipEvent_t pool_ev = nullptr;  // on the upload stream
   bool pool_ev_pending = false;
   // host-side phase times of the last single-object call (ecamd_call_phases):
   // [0] copy in, [1] launch, [2] host work beside the kernel, [3] wait for
@@ -582,10 +580,12 @@ struct Instance {
   // call, BENCH_r04 decode_fresh_ms).  The slot's buffers are rewritten only
   // after ring_acquire's wait for the launch that read them, which ran after
   // this copy.
+  hipError_t ensure_ustream() {
+    return ustream ? hipSuccess : hipStreamCreateWithFlags(&ustream, hipStreamNonBlocking);
+  }
   hipError_t ring_commit(RingSlot* r, size_t n, hipStream_t s) {
-    hipError_t e = hipSuccess;
-    if (!ustream && (e = hipStreamCreateWithFlags(&ustream, hipStreamNonBlocking)) != hipSuccess)
-      return e;
+    hipError_t e = ensure_ustream();
+    if (e != hipSuccess) return e;
     if (!r->cev && (e = hipEventCreateWithFlags(&r->cev, hipEventDisableTiming)) != hipSuccess)
       return e;
     if ((e = hipMemcpyAsync(r->dev.p, r->host, n, hipMemcpyHostToDevice, ustream)) != hipSuccess)
@@ -904,7 +904,6 @@ hipError_t pool_recycle(Instance& I, hipStream_t s) {
   if (!I.pool_gen_ev && (e = hipEventCreateWithFlags(&I.pool_gen_ev, hipEventDisableTiming)) != hipSuccess)
     return e;
   if ((e = hipEventRecord(I.pool_gen_ev, s)) != hipSuccess) return e;
-  I.pool_gen_stream = s;
   I.pool_gen_pending = true;
   I.pool_index.clear();
   I.pool_used = 0;
@@ -957,50 +956,52 @@ int pool_slot(Instance& I, uint32_t avail_mask, const int* avail, int dest, uint
   return 0;
 }
 
-// Upload the table sets staged by pool_slot (one async copy through the ring
-// on the launch stream: no kernel reads a new slot before the copy, and no
-// queued kernel reads it at all -- slots are only rewritten after the pool's
-// recycle, whose event a copy on another stream waits for).  Call before
-// every launch that reads the pool.
+// Upload the table sets staged by pool_slot (one async copy through the ring)
+// and order the launch about to be queued on `stream` after every table copy
+// so far.  Call before every launch that reads the pool.
 //
-// pool_ev marks the last table copy.  A launch on another stream waits for
-// it; a copy on another stream first waits for the previous copy too, so
-// each new record covers every copy before it (a later launch that reads
-// slots of both copies waits for one event).  (Round-3 advisor: without that
-// wait, a stream reusing a pattern staged by another stream's still-running
-// copy could read its slot before the copy landed.)
+// Every table copy runs on the instance's upload stream, in order (round 5:
+// they had run on the launch stream, where each one sat between two kernels;
+// decode with erasure masks new every call brings new patterns now and then,
+// pyeclib_c.c:878).  A copy that rewrites slots after a recycle first waits
+// for the recycle's marker (pool_gen_ev, recorded behind every launch that
+// could read the old sets); pool_ev marks the last copy, and a launch on any
+// stream waits for it until it is known to be complete.  No kernel reads a
+// slot before its copy, and no queued kernel reads a slot being rewritten.
 hipError_t pool_commit(Instance& I, hipStream_t stream) {
   hipError_t e = hipSuccess;
-  const bool other_pending = I.pool_ev_pending && I.pool_ev_stream != stream &&
-                             hipEventQuery(I.pool_ev) != hipSuccess;
-  if (I.pool_ev_pending && !other_pending && I.pool_ev_stream != stream) I.pool_ev_pending = false;
   if (!I.pool_stage.empty()) {
-    if (I.pool_gen_pending && I.pool_gen_stream != stream) {
+    if ((e = I.ensure_ustream()) != hipSuccess) return e;
+    if (I.pool_gen_pending) {
       if (hipEventQuery(I.pool_gen_ev) == hipSuccess)
         I.pool_gen_pending = false;
-      else if ((e = hipStreamWaitEvent(stream, I.pool_gen_ev, 0)) != hipSuccess)
+      else if ((e = hipStreamWaitEvent(I.ustream, I.pool_gen_ev, 0)) != hipSuccess)
         return e;
     }
-    if (other_pending && (e = hipStreamWaitEvent(stream, I.pool_ev, 0)) != hipSuccess) return e;
     const size_t n = I.pool_stage.size();
     RingSlot* r = I.ring_acquire(n, &e);
     if (!r) return e;
     std::memcpy(r->host, I.pool_stage.data(), n);
     const size_t slot_bytes = I.table_bytes() * I.passes;
     e = hipMemcpyAsync(I.pool.b() + static_cast<size_t>(I.pool_stage_first) * slot_bytes, r->host,
-                       n, hipMemcpyHostToDevice, stream);
+                       n, hipMemcpyHostToDevice, I.ustream);
     I.pool_stage.clear();
-    const hipError_t er = I.ring_release(r, stream);
     if (e != hipSuccess) return e;
-    if (er != hipSuccess) return er;
     if (!I.pool_ev && (e = hipEventCreateWithFlags(&I.pool_ev, hipEventDisableTiming)) != hipSuccess)
       return e;
-    if ((e = hipEventRecord(I.pool_ev, stream)) != hipSuccess) return e;
-    I.pool_ev_stream = stream;
+    if ((e = hipEventRecord(I.pool_ev, I.ustream)) != hipSuccess) return e;
     I.pool_ev_pending = true;
-    return hipSuccess;
+    // the launch waits for the copy; the slot's host buffer is reused only
+    // after a marker on `stream` behind that wait
+    if ((e = hipStreamWaitEvent(stream, I.pool_ev, 0)) != hipSuccess) return e;
+    return I.ring_release(r, stream);
   }
-  if (other_pending) e = hipStreamWaitEvent(stream, I.pool_ev, 0);
+  if (I.pool_ev_pending) {
+    if (hipEventQuery(I.pool_ev) == hipSuccess)
+      I.pool_ev_pending = false;
+    else
+      e = hipStreamWaitEvent(stream, I.pool_ev, 0);
+  }
   return e;
 }
 
