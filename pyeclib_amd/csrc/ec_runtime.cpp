@@ -1685,8 +1685,10 @@ struct CallerPin {
 // products are per position, so a window is an encode / decode of its own
 // over a "virtual object" of k slices of wl bytes -- the host stages window
 // w + 1 (the worker pool) while the GPU runs window w.  Objects from
-// kWindowMin on, kWindows windows of whole 4 KiB tiles.
-constexpr uint64_t kWindowMin = uint64_t(1) << 20;
+// kWindowMin on, kWindows windows of whole 4 KiB tiles.  (Measured, r05h:
+// at 1 MiB the pool's wake-up per window made the encode slower, 82 -> 146
+// us; hence the 2 MiB floor.)
+constexpr uint64_t kWindowMin = uint64_t(2) << 20;
 constexpr uint64_t kWindows = 4;
 inline uint64_t window_bytes(uint64_t bs) {
   return ((bs + kWindows - 1) / kWindows + 4095) & ~uint64_t(4095);
@@ -1701,10 +1703,11 @@ inline uint64_t window_bytes(uint64_t bs) {
 // copies the parity out.  Objects past the single_pinned_max knob that do not
 // register take DMA copies through HBM instead.
 // encode_into in windows (see kWindowMin): window w's virtual object (slice
-// j = object bytes [j bs + w0, + wl), zero past len) is staged at `vobj`
-// while the data fragments take the same bytes in the same pass, its parity
-// rows land at payload offset w0 of the staged parity fragments.  Returns 1
-// (nothing done) when the staging buffer is not available.
+// j = object bytes [j bs + w0, + wl), zero past len) is staged at `vobj` and
+// launched, its parity rows landing at payload offset w0 of the staged
+// parity fragments; once every window is queued, the data fragments are
+// copied from the object while the GPU works.  Returns 1 (nothing done) when
+// the staging buffer is not available.
 int encode_windows(Instance& I, const char* data, uint64_t len, uint8_t* const* frags, uint64_t bs,
                    PhaseClock& clk) {
   const int k = I.k, m = I.m;
@@ -1724,15 +1727,8 @@ int encode_windows(Instance& I, const char* data, uint64_t len, uint8_t* const* 
       const uint64_t at = static_cast<uint64_t>(j) * bs + w0;
       const uint64_t c = at < len ? std::min(wl, len - at) : 0;
       uint8_t* v = vobj + static_cast<uint64_t>(j) * wl;
-      uint8_t* f = frags[j] + kHeaderBytes + w0;
-      if (c) {
-        jobs.push_back({v, data + at, c});
-        jobs.push_back({f, data + at, c});
-      }
-      if (c < wl) {
-        jobs.push_back({v + c, nullptr, wl - c});
-        jobs.push_back({f + c, nullptr, wl - c});
-      }
+      if (c) jobs.push_back({v, data + at, c});
+      if (c < wl) jobs.push_back({v + c, nullptr, wl - c});
     }
     host_copy(jobs.data(), static_cast<int>(jobs.size()), true);
     const int rc = run_encode(I, vobj, static_cast<uint64_t>(k) * wl, static_cast<uint64_t>(k) * wl,
@@ -1743,6 +1739,15 @@ int encode_windows(Instance& I, const char* data, uint64_t len, uint8_t* const* 
     }
   }
   clk.mark(1);
+  jobs.clear();  // the data fragments: the object's slices, zero padded
+  for (int j = 0; j < k; ++j) {
+    const uint64_t at = static_cast<uint64_t>(j) * bs;
+    const uint64_t c = at < len ? std::min(bs, len - at) : 0;
+    if (c) jobs.push_back({frags[j] + kHeaderBytes, data + at, c});
+    if (c < bs) jobs.push_back({frags[j] + kHeaderBytes + c, nullptr, bs - c});
+  }
+  host_copy(jobs.data(), static_cast<int>(jobs.size()));
+  clk.mark(2);
   hipError_t e;
   if ((e = hipStreamSynchronize(I.stream)) != hipSuccess) return hip_errno(e);
   clk.mark(3);

@@ -361,12 +361,12 @@ def _check_batch_crc(oracle, gpu, ec_type, k, m, obj_len, n_obj, legacy):
 # ---------------- single-object calls in position windows (objects >= 1 MiB) ----------------
 
 @pytest.mark.parametrize("ec_type,k,m,n", [
-    ("liberasurecode_rs_vand", 10, 4, (1 << 20) + 2), ("amd_rs_vand", 12, 6, 3 * (1 << 20) + 7),
-    ("amd_rs_vand", 6, 9, (2 << 20) + 1), ("amd_rs_vand", 3, 5, (1 << 20) + 33),
+    ("liberasurecode_rs_vand", 10, 4, (2 << 20) + 2), ("amd_rs_vand", 12, 6, 3 * (1 << 20) + 7),
+    ("amd_rs_vand", 6, 9, (2 << 20) + 1), ("amd_rs_vand", 3, 5, (2 << 20) + 33),
     ("amd_rs_vand", 28, 4, 5 * (1 << 20) + 9), ("isa_l_rs_cauchy", 12, 4, (4 << 20) + 5),
-    ("isa_l_rs_vand", 8, 3, (1 << 20) + 1)])
+    ("isa_l_rs_vand", 8, 3, (2 << 20) + 1), ("liberasurecode_rs_vand", 10, 4, 4 << 20)])
 def test_single_object_windows(oracle, ec_type, k, m, n):
-    """Single-object encode / decode / reconstruct of objects from 1 MiB on,
+    """Single-object encode / decode / reconstruct of objects from 2 MiB on,
     which run as kWindows windows of payload positions (ec_runtime.cpp
     encode_windows / decode_windows), multi-pass parity and multi-pass decode
     (m > 4) included: fragments and decoded bytes against the oracle."""
