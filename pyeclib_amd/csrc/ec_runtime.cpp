@@ -1677,23 +1677,6 @@ struct CallerPin {
   ~CallerPin() { (void)unpin(); }  // error paths, after their stream synchronize
 };
 
-// Single-object calls in payload-position windows (round 5).  With the
-// caller's buffers copied through the pinned staging buffer (registration is
-// opt-in, section 6b of DESIGN.md), a whole-object call runs copy-in, kernel
-// and copy-out one after the other.  Cut into windows of positions instead --
-// window w holds bytes [w0, w0 + wl) of every fragment payload, and GF
-// products are per position, so a window is an encode / decode of its own
-// over a "virtual object" of k slices of wl bytes -- the host stages window
-// w + 1 (the worker pool) while the GPU runs window w.  Objects from
-// kWindowMin on, kWindows windows of whole 4 KiB tiles.  (Measured, r05h:
-// at 1 MiB the pool's wake-up per window made the encode slower, 82 -> 146
-// us; hence the 2 MiB floor.)
-constexpr uint64_t kWindowMin = uint64_t(2) << 20;
-constexpr uint64_t kWindows = 4;
-inline uint64_t window_bytes(uint64_t bs) {
-  return ((bs + kWindows - 1) / kWindows + 4095) & ~uint64_t(4095);
-}
-
 // liberasurecode_encode's work for one object, into k + m caller-provided
 // fragments of bs + 80 bytes (caller holds I.mu, device set).  The kernel
 // reads the caller's object in place over PCIe (CallerPin) -- or, when it
@@ -1702,63 +1685,6 @@ inline uint64_t window_bytes(uint64_t bs) {
 // fragments from the object (prepare_fragments_for_encode's copy), then
 // copies the parity out.  Objects past the single_pinned_max knob that do not
 // register take DMA copies through HBM instead.
-// encode_into in windows (see kWindowMin): window w's virtual object (slice
-// j = object bytes [j bs + w0, + wl), zero past len) is staged at `vobj` and
-// launched, its parity rows landing at payload offset w0 of the staged
-// parity fragments; once every window is queued, the data fragments are
-// copied from the object while the GPU works.  Returns 1 (nothing done) when
-// the staging buffer is not available.
-int encode_windows(Instance& I, const char* data, uint64_t len, uint8_t* const* frags, uint64_t bs,
-                   PhaseClock& clk) {
-  const int k = I.k, m = I.m;
-  const uint64_t win = window_bytes(bs);
-  const uint64_t nwin = (bs + win - 1) / win;
-  const uint64_t fs = round16(kHeaderBytes + round16(bs));
-  const uint64_t vbytes = static_cast<uint64_t>(k) * win;
-  uint8_t* pin = I.pin.ensure(nwin * vbytes + fs * m);
-  if (!pin) return 1;
-  uint8_t* d_par = pin + nwin * vbytes;
-  thread_local std::vector<CopyJob> jobs;
-  for (uint64_t w = 0; w < nwin; ++w) {
-    const uint64_t w0 = w * win, wl = std::min(win, bs - w0);
-    uint8_t* vobj = pin + w * vbytes;
-    jobs.clear();
-    for (int j = 0; j < k; ++j) {
-      const uint64_t at = static_cast<uint64_t>(j) * bs + w0;
-      const uint64_t c = at < len ? std::min(wl, len - at) : 0;
-      uint8_t* v = vobj + static_cast<uint64_t>(j) * wl;
-      if (c) jobs.push_back({v, data + at, c});
-      if (c < wl) jobs.push_back({v + c, nullptr, wl - c});
-    }
-    host_copy(jobs.data(), static_cast<int>(jobs.size()), true);
-    const int rc = run_encode(I, vobj, static_cast<uint64_t>(k) * wl, static_cast<uint64_t>(k) * wl,
-                              1, d_par + w0, nullptr, fs, fs * m, false, I.stream);
-    if (rc < 0) {
-      (void)hipStreamSynchronize(I.stream);
-      return rc;
-    }
-  }
-  clk.mark(1);
-  jobs.clear();  // the data fragments: the object's slices, zero padded
-  for (int j = 0; j < k; ++j) {
-    const uint64_t at = static_cast<uint64_t>(j) * bs;
-    const uint64_t c = at < len ? std::min(bs, len - at) : 0;
-    if (c) jobs.push_back({frags[j] + kHeaderBytes, data + at, c});
-    if (c < bs) jobs.push_back({frags[j] + kHeaderBytes + c, nullptr, bs - c});
-  }
-  host_copy(jobs.data(), static_cast<int>(jobs.size()));
-  clk.mark(2);
-  hipError_t e;
-  if ((e = hipStreamSynchronize(I.stream)) != hipSuccess) return hip_errno(e);
-  clk.mark(3);
-  jobs.clear();
-  for (int p = 0; p < m; ++p)
-    jobs.push_back({frags[k + p] + kHeaderBytes, d_par + p * fs + kHeaderBytes, bs});
-  host_copy(jobs.data(), static_cast<int>(jobs.size()));
-  clk.mark(4);
-  return 0;
-}
-
 int encode_into(Instance& I, const char* data, uint64_t len, uint8_t* const* frags) {
   const int k = I.k, m = I.m;
   PhaseClock clk(I.phase_us);
@@ -1777,13 +1703,7 @@ int encode_into(Instance& I, const char* data, uint64_t len, uint8_t* const* fra
     }
     host_copy(jobs.data(), static_cast<int>(jobs.size()));
   };
-  int wrc = 1;
-  if (bs > 0 && len >= kWindowMin && len <= I.knobs.single_pinned_max && !I.knobs.register_caller)
-    wrc = encode_windows(I, data, len, frags, bs, clk);
-  if (wrc < 0) return wrc;
-  if (wrc == 0) {
-    // windows done: data fragments and parity are in place
-  } else if (bs > 0) {
+  if (bs > 0) {
     const uint64_t fs = round16(kHeaderBytes + round16(bs));
     const uint64_t obj_bytes = round16(len);
     // the object in place when it registers (through round16(len): the edge
@@ -2007,63 +1927,6 @@ int decode_prepare(Instance& I, char** frags, int n, uint64_t fragment_len, int 
   return 0;
 }
 
-// decode_into in windows (see kWindowMin): window w's inputs -- the first k
-// available fragments' payload bytes [w0, w0 + wl), compact -- are staged
-// while the GPU decodes window w - 1 into its virtual object, whose slices
-// are copied to the object at the end.  Returns 1 (nothing done) when the
-// staging buffer is not available.
-int decode_windows(Instance& I, const DecodeIn& D, uint8_t* out, PhaseClock& clk) {
-  const int k = I.k;
-  const uint64_t bs = D.bs, orig = D.orig;
-  const uint64_t win = window_bytes(bs);
-  const uint64_t nwin = (bs + win - 1) / win;
-  const uint64_t fsw = round16(kHeaderBytes + win);
-  const uint64_t in_bytes = fsw * k, ob = static_cast<uint64_t>(k) * win;
-  uint8_t* pin = I.pin.ensure(nwin * (in_bytes + ob));
-  if (!pin) return 1;
-  // the first k available fragments in index order (the rs_vand choice)
-  const uint8_t* src[kMaxFragments];
-  uint32_t mask = 0;
-  int c = 0;
-  for (int i = 0; i < k + I.m && c < k; ++i)
-    if (D.P.by_idx[i]) {
-      src[c++] = D.P.by_idx[i] + kHeaderBytes;
-      mask |= 1u << i;
-    }
-  if (c < k) return -EINSUFFFRAGS;
-  thread_local std::vector<CopyJob> jobs;
-  for (uint64_t w = 0; w < nwin; ++w) {
-    const uint64_t w0 = w * win, wl = std::min(win, bs - w0);
-    uint8_t* vin = pin + w * (in_bytes + ob);
-    jobs.clear();
-    for (int j = 0; j < k; ++j) jobs.push_back({vin + j * fsw + kHeaderBytes, src[j] + w0, wl});
-    host_copy(jobs.data(), static_cast<int>(jobs.size()), true);
-    DecodeJob J{vin, fsw, in_bytes, static_cast<uint64_t>(k) * wl, vin + in_bytes,
-                static_cast<uint64_t>(k) * wl, 1, &mask, nullptr, nullptr, true};
-    const int rc = run_decode(I, J, I.stream);
-    if (rc < 0) {
-      (void)hipStreamSynchronize(I.stream);
-      return rc;
-    }
-  }
-  clk.mark(1);
-  const hipError_t e = hipStreamSynchronize(I.stream);
-  if (e != hipSuccess) return hip_errno(e);
-  clk.mark(3);
-  jobs.clear();
-  for (uint64_t w = 0; w < nwin; ++w) {
-    const uint64_t w0 = w * win, wl = std::min(win, bs - w0);
-    const uint8_t* vout = pin + w * (in_bytes + ob) + in_bytes;
-    for (int j = 0; j < k; ++j) {
-      const uint64_t at = static_cast<uint64_t>(j) * bs + w0;
-      if (at < orig) jobs.push_back({out + at, vout + j * wl, std::min(wl, orig - at)});
-    }
-  }
-  host_copy(jobs.data(), static_cast<int>(jobs.size()));
-  clk.mark(4);
-  return 0;
-}
-
 // Decode into `out` (D.orig bytes; caller holds I.mu, device set).
 int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
   const int k = I.k;
@@ -2083,10 +1946,6 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
     host_copy(jobs.data(), static_cast<int>(jobs.size()));
     clk.mark(4);
     return 0;
-  }
-  if (orig >= kWindowMin && orig <= I.knobs.single_pinned_max && !I.knobs.register_caller) {
-    const int wrc = decode_windows(I, D, out, clk);
-    if (wrc <= 0) return wrc;
   }
   const uint64_t fs = round16(kHeaderBytes + round16(bs));
   const uint64_t obj_bytes = round16(orig);

@@ -113,10 +113,10 @@ Pool& pool() {
 
 int host_copy_threads() { return threads_from_env(); }
 
-void host_copy(const CopyJob* jobs, int count, bool parallel) {
+void host_copy(const CopyJob* jobs, int count) {
   size_t total = 0;
   for (int i = 0; i < count; ++i) total += jobs[i].n;
-  if ((total < kParallelMin && !(parallel && total >= 2 * kPiece)) || !pool().usable()) {
+  if (total < kParallelMin || !pool().usable()) {
     for (int i = 0; i < count; ++i)
       run_piece({static_cast<uint8_t*>(jobs[i].dst), static_cast<const uint8_t*>(jobs[i].src),
                  jobs[i].n});

@@ -23,10 +23,8 @@ struct CopyJob {
   size_t n;
 };
 
-// Run every job (any mix of copies and zero-fills) and return when all are
-// done.  `parallel`: use the pool whatever the total (the caller knows the
-// pool's wake-up is paid for, e.g. copies that feed a waiting GPU).
-void host_copy(const CopyJob* jobs, int count, bool parallel = false);
+// Run every job (any mix of copies and zero-fills) and return when all are done.
+void host_copy(const CopyJob* jobs, int count);
 
 inline void host_copy(void* dst, const void* src, size_t n) {
   const CopyJob j{dst, src, n};
