@@ -1,5 +1,6 @@
 #include "host_copy.hpp"
 
+#include <sched.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -98,9 +99,18 @@ class Pool {
   std::atomic<size_t> next_{0}, done_{0};
 };
 
+// Default: a quarter of the CPUs this process may run on, 2..8 (round 5,
+// MI355X box: 8 workers took a 4 MiB encode / decode call from 227 / 224 us
+// to 198 / 196 us against 4 workers)
+int default_threads() {
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) != 0) return 4;
+  return std::max(2, std::min(CPU_COUNT(&set) / 4, 8));
+}
+
 int threads_from_env() {
   const char* v = std::getenv("ECAMD_COPY_THREADS");
-  const int n = (v == nullptr || *v == 0) ? 4 : std::atoi(v);
+  const int n = (v == nullptr || *v == 0) ? default_threads() : std::atoi(v);
   return std::max(0, std::min(n, 32));
 }
 

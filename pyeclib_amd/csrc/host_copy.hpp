@@ -31,7 +31,8 @@ inline void host_copy(void* dst, const void* src, size_t n) {
   host_copy(&j, 1);
 }
 
-// Worker threads of the pool (ECAMD_COPY_THREADS, read once; default 4,
+// Worker threads of the pool (ECAMD_COPY_THREADS, read once; default a
+// quarter of the CPUs in the affinity mask, 2..8,
 // 0 = the calling thread only).
 int host_copy_threads();
 
