@@ -598,6 +598,40 @@ def reference_cli_bench(iterations=200, oracle_iterations=20):
     return {"reference_cli_bench": out}
 
 
+# ---------------- first calls of a fresh process ----------------
+
+_FIRST_CALL = r"""
+import json, os, time
+t0 = time.perf_counter()
+import pyeclib_amd
+t1 = time.perf_counter()
+d = pyeclib_amd.ECDriver(k=10, m=4, ec_type="liberasurecode_rs_vand")
+t2 = time.perf_counter()
+data = os.urandom(1 << 20)
+r = {"import_ms": t1 - t0, "driver_ms": t2 - t1}
+for i in (1, 2):
+    t = time.perf_counter(); frags = d.encode(data); r[f"encode_{i}_ms"] = time.perf_counter() - t
+for i in (1, 2):
+    t = time.perf_counter(); back = d.decode(frags[4:]); r[f"decode_{i}_ms"] = time.perf_counter() - t
+assert back == data
+print(json.dumps({k: round(v * 1e3, 2) for k, v in r.items()}))
+"""
+
+
+def first_call():
+    """What a fresh process pays before its first results (round 5, verdict
+    item 6): import, ECDriver construction (HIP initialisation, device
+    tables), then the first and second 1 MiB encode and decode (the first
+    launch of each kernel loads its code object).  A child interpreter, so
+    nothing of this process's warm state counts."""
+    text = subprocess.run([sys.executable, "-c", _FIRST_CALL], cwd=ROOT, capture_output=True,
+                          text=True, timeout=300, check=True).stdout
+    out = json.loads(text.strip().splitlines()[-1])
+    out["note"] = ("fresh interpreter: import pyeclib_amd, ECDriver(10, 4) construction, then the "
+                   "first and second 1 MiB encode and decode (4 data fragments missing), wall ms")
+    return {"first_call": out}
+
+
 # ---------------- configs[0]: the file CLI on k=4 m=2 ----------------
 
 def config0_cli(args, size=1 << 20, reps=5):
@@ -684,7 +718,7 @@ def config0_cli(args, size=1 << 20, reps=5):
 
 # ---------------- decode with erasures that change every step ----------------
 
-def fresh_decode_steady(args, codec, stripes, objs, out, stream, B, rank):
+def fresh_decode_steady(args, codec, stripes, objs, out, stream, B, rank, head_masks):
     """Decode with erasures drawn anew for every call, back to back: the
     masks of all `--fresh-steps` calls are drawn first (outside the clock),
     then the calls are made with no synchronisation between them, so call
@@ -694,23 +728,26 @@ def fresh_decode_steady(args, codec, stripes, objs, out, stream, B, rank):
     would run.  Reported per call: GPU event span / calls, and host wall /
     calls.  Every call decodes the same objects, so the last call's output is
     compared with them; each call's output is also checked, against the
-    objects, by the idle-GPU variant (fresh_decode)."""
+    objects, by the idle-GPU variant (fresh_decode).  A third pass makes the
+    same calls with the headline's masks every time (the control: the same
+    back-to-back shape, no new masks)."""
     import torch
     k, m, n = args.k, args.m, args.obj_bytes
     steps = max(2, args.fresh_steps)
 
-    def run(first):  # `steps` calls, masks new for every call
+    def run(first, fixed=None):  # `steps` calls, masks new for every call (or `fixed`)
         all_masks = []
         for i in range(first, first + steps):
             rng = np.random.Generator(np.random.PCG64(SEED + rank + 7919 * (i + 1)))
-            all_masks.append(erasure_masks(rng, B, k, m, args.erasures))
+            all_masks.append(erasure_masks(rng, B, k, m, args.erasures) if fixed is None
+                             else fixed)
         out.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         # one extra call ahead of the clock: the span then starts with the
         # pipeline full (call i+1's host work under call i's kernel), not
         # with the GPU idle through the first call's host work
-        codec.decode(stripes, n, erasure_masks(
+        codec.decode(stripes, n, fixed if fixed is not None else erasure_masks(
             np.random.Generator(np.random.PCG64(SEED + rank + 104729 + first)), B, k, m,
             args.erasures), out)
         e0.record(stream)
@@ -727,7 +764,11 @@ def fresh_decode_steady(args, codec, stripes, objs, out, stream, B, rank):
     # second pass: new masks again, their patterns mostly cached
     cold_ms, cold_wall, ok0 = run(0)
     ms, wall_ms, ok1 = run(steps)
+    rep_ms, rep_wall, ok2 = run(0, head_masks)
     return {"decode_fresh_ms": round(ms, 4),
+            "decode_repeat_ms": round(rep_ms, 4),
+            "decode_repeat_wall_ms": round(rep_wall, 4),
+            "decode_fresh_vs_repeat": round(ms / rep_ms, 4),
             "decode_fresh_wall_ms": round(wall_ms, 4),
             "decode_fresh_cold_ms": round(cold_ms, 4),
             "decode_fresh_cold_wall_ms": round(cold_wall, 4),
@@ -741,8 +782,10 @@ def fresh_decode_steady(args, codec, stripes, objs, out, stream, B, rank):
                                  "such pass, "
                                  "whose patterns are mostly new to the device's table pool, "
                                  "decode_fresh_ms = the next pass (new masks, patterns mostly "
-                                 "cached); both passes' last outputs compared with the objects"}, \
-        ok0 and ok1
+                                 "cached); both passes' last outputs compared with the objects; "
+                                 "decode_repeat_ms = the same back-to-back pass with the "
+                                 "headline's masks in every call (the control)"}, \
+        ok0 and ok1 and ok2
 
 
 def fresh_decode(args, codec, stripes, objs, out, stream, B, rank):
@@ -991,7 +1034,8 @@ def main():
     if two == "decode" and args.fresh_steps > 0:
         fresh, fresh_ok = fresh_decode(args, codec, stripes, objs, out, stream, B, rank)
         result.update(fresh)
-        steady, steady_ok = fresh_decode_steady(args, codec, stripes, objs, out, stream, B, rank)
+        steady, steady_ok = fresh_decode_steady(args, codec, stripes, objs, out, stream, B, rank,
+                                                masks)
         result.update(steady)
         fresh_ok = fresh_ok and steady_ok
         # the headline batch is decoded again so the oracle check below sees it
@@ -1060,6 +1104,10 @@ def main():
             result.update(reference_cli_bench())
         except Exception as exc:  # noqa: BLE001 -- an auxiliary leg: recorded, not fatal
             result["reference_cli_bench"] = {"error": repr(exc)}
+        try:
+            result.update(first_call())
+        except Exception as exc:  # noqa: BLE001 -- an auxiliary leg: recorded, not fatal
+            result["first_call"] = {"error": repr(exc)}
     if rank == 0 and world == 1 and args.swift_procs and not args.no_host and w == 16:
         # the Swift call shape: P processes, one ECDriver call per segment
         # (this process holds the GPU too: at most 15 workers beside it)

@@ -126,6 +126,14 @@ struct Knobs {
   int host_streams = 3;         // ECAMD_HOST_STREAMS
   int host_chunk_mb = 32;       // ECAMD_HOST_CHUNK_MB
   bool edge_blocks = true;      // ECAMD_EDGE_BLOCKS=0: the round-2 launch form
+  // ECAMD_UPLOAD_HOST_WAIT=0: a launch waits for its descriptor upload on the
+  // GPU (hipStreamWaitEvent) instead of the host waiting for the copy before
+  // the launch.  Round 5 (tools/timeline_gaps.py on fresh_probe.py's
+  // back-to-back decodes with new masks per call): the GPU-side wait opened
+  // an 11.6 us gap before every kernel, although each copy had long finished;
+  // repeated masks (no upload) ran back to back with none.  The host is ahead
+  // of the GPU there, so its wait for a 16 KiB copy costs nothing.
+  bool upload_host_wait = true;
   static Knobs from_env() {
     Knobs k;
     k.single_pinned_max = static_cast<size_t>(
@@ -137,6 +145,7 @@ struct Knobs {
     k.host_chunk_mb = static_cast<int>(std::max<long>(1, env_long("ECAMD_HOST_CHUNK_MB", k.host_chunk_mb)));
     k.edge_blocks = env_on("ECAMD_EDGE_BLOCKS", true);
     k.register_caller = env_on("ECAMD_REGISTER_CALLER", false);
+    k.upload_host_wait = env_on("ECAMD_UPLOAD_HOST_WAIT", true);
     return k;
   }
 };
@@ -558,7 +567,11 @@ struct Instance {
       r.pending = false;
       if (*err != hipSuccess) return nullptr;
     }
-    if (!r.ev && (*err = hipEventCreateWithFlags(&r.ev, hipEventDisableTiming)) != hipSuccess)
+    // the slot's event only says that the launches reading its device bytes
+    // have finished (nothing they wrote is read through it): no system-scope
+    // fence, whose cache writeback cost a few us between kernels (round 5)
+    if (!r.ev && (*err = hipEventCreateWithFlags(
+                      &r.ev, hipEventDisableTiming | hipEventDisableSystemFence)) != hipSuccess)
       return nullptr;
     if (r.cap < n) {
       if (r.host) (void)hipHostFree(r.host);
@@ -591,6 +604,7 @@ struct Instance {
     if ((e = hipMemcpyAsync(r->dev.p, r->host, n, hipMemcpyHostToDevice, ustream)) != hipSuccess)
       return e;
     if ((e = hipEventRecord(r->cev, ustream)) != hipSuccess) return e;
+    if (knobs.upload_host_wait) return hipEventSynchronize(r->cev);
     return hipStreamWaitEvent(s, r->cev, 0);
   }
   hipError_t ring_release(RingSlot* r, hipStream_t s) {
@@ -972,11 +986,14 @@ hipError_t pool_commit(Instance& I, hipStream_t stream) {
   hipError_t e = hipSuccess;
   if (!I.pool_stage.empty()) {
     if ((e = I.ensure_ustream()) != hipSuccess) return e;
+    bool behind_gpu = false;  // the copy waits for queued kernels (pool recycled)
     if (I.pool_gen_pending) {
       if (hipEventQuery(I.pool_gen_ev) == hipSuccess)
         I.pool_gen_pending = false;
       else if ((e = hipStreamWaitEvent(I.ustream, I.pool_gen_ev, 0)) != hipSuccess)
         return e;
+      else
+        behind_gpu = true;
     }
     const size_t n = I.pool_stage.size();
     RingSlot* r = I.ring_acquire(n, &e);
@@ -990,6 +1007,11 @@ hipError_t pool_commit(Instance& I, hipStream_t stream) {
     if (!I.pool_ev && (e = hipEventCreateWithFlags(&I.pool_ev, hipEventDisableTiming)) != hipSuccess)
       return e;
     if ((e = hipEventRecord(I.pool_ev, I.ustream)) != hipSuccess) return e;
+    if (I.knobs.upload_host_wait && !behind_gpu) {
+      // as ring_commit: the host waits for the copy, the launch needs no wait
+      if ((e = hipEventSynchronize(I.pool_ev)) != hipSuccess) return e;
+      return I.ring_release(r, stream);
+    }
     I.pool_ev_pending = true;
     // the launch waits for the copy; the slot's host buffer is reused only
     // after a marker on `stream` behind that wait

@@ -390,3 +390,49 @@ def test_single_object_large(oracle, ec_type, k, m, n):
         assert drv.decode(avail) == data
         assert drv.reconstruct(avail, lost[:2]) == [frags[i] for i in lost[:2]]
     drv.close()
+
+
+@pytest.mark.parametrize("n_obj,obj_len", [(64, 4 << 20), (7, 300001)])
+def test_back_to_back_calls_with_erased_bytes(gpu, n_obj, obj_len):
+    """Decodes and reconstructs issued back to back with no synchronisation,
+    each call with new erasure masks over its own copy of the stripes whose
+    erased fragments are ZEROED: a call that ran with another call's
+    descriptors or table sets (the upload ring, the host-side upload waits,
+    round 5) would read zeros and differ.  The batch tests' stripes keep every
+    fragment intact, so any valid pattern decodes them -- they cannot see
+    that.  64 x 4 MiB takes the loader / consumer decode, 7 x 300 KB the
+    stream kernels."""
+    import torch
+    from pyeclib_amd import batch
+    k, m, rounds = 10, 4, 8
+    codec = batch.BatchCodec(k, m)
+    bs, obj_stride, frag_stride = _batch_layout(k, m, n_obj, obj_len)
+    g = torch.Generator(device="cpu").manual_seed(obj_len)
+    objs = torch.randint(0, 256, (n_obj, obj_stride), dtype=torch.uint8, generator=g).to(gpu)
+    frags = torch.zeros((n_obj, k + m, frag_stride), dtype=torch.uint8, device=gpu)
+    codec.encode(objs, obj_len, parity=frags[:, k:], data=frags[:, :k])
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(n_obj)
+    jobs = []
+    for r in range(rounds):
+        lost = [rng.choice(k + m, int(rng.integers(1, m + 1)), replace=False) for _ in range(n_obj)]
+        masks = [sum(1 << i for i in range(k + m) if i not in ls) for ls in lost]
+        st = frags.clone()
+        gone = torch.zeros((n_obj, k + m), dtype=torch.bool)
+        for o, ls in enumerate(lost):
+            gone[o, torch.as_tensor(ls)] = True
+        st[gone.to(gpu)] = 0
+        out = torch.zeros((n_obj, obj_stride), dtype=torch.uint8, device=gpu)
+        dest = [int(ls[0]) for ls in lost]
+        rec = torch.zeros((n_obj, frag_stride), dtype=torch.uint8, device=gpu)
+        jobs.append((st, masks, out, dest, rec))
+    torch.cuda.synchronize()
+    for st, masks, out, dest, rec in jobs:  # no synchronisation between the calls
+        codec.decode(st, obj_len, masks, out)
+        codec.reconstruct(st, obj_len, masks, dest, rec)
+    torch.cuda.synchronize()
+    fl = 80 + bs
+    for r, (st, masks, out, dest, rec) in enumerate(jobs):
+        assert torch.equal(out[:, :obj_len], objs[:, :obj_len]), f"round {r} decode"
+        want = frags[torch.arange(n_obj, device=gpu), torch.as_tensor(dest, device=gpu), :fl]
+        assert torch.equal(rec[:, :fl], want), f"round {r} reconstruct"
