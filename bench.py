@@ -97,6 +97,9 @@ def parse(argv=None):
                          "GPU reaches its steady clocks (the kernel times fall by up to 25 %% "
                          "over the first ~20 ms of load: profiles/r03q_bench_*.json step_ms); "
                          "0 = off.  Reported as `settle` in the JSON line")
+    ap.add_argument("--events", choices=("nofence", "torch"), default="nofence",
+                    help="timing events of the timed steps: HIP events without the system-scope "
+                         "fence (default) or torch.cuda.Event")
     ap.add_argument("--fresh-steps", type=int, default=8,
                     help="decode steps whose erasure masks are new every step (drawn from "
                          "the seed outside the clock, handed over inside it): timed apart "
@@ -398,6 +401,39 @@ def cpu_model() -> str:
     except OSError:
         pass
     return "unknown"
+
+
+class HipEvent:
+    """A HIP timing event without the system-scope fence
+    (hipEventDisableSystemFence), recorded on the launch stream by handle:
+    torch.cuda.Event's record writes back the caches between the two kernels
+    it separates, a cost the timed steps would otherwise carry twice per step
+    (round 5).  Same interface as torch.cuda.Event for record/elapsed_time."""
+    _hip = None
+
+    def __init__(self):
+        if HipEvent._hip is None:
+            HipEvent._hip = ctypes.CDLL("libamdhip64.so")
+        self.h = ctypes.c_void_p()
+        rc = HipEvent._hip.hipEventCreateWithFlags(ctypes.byref(self.h), ctypes.c_uint(0x20000000))
+        if rc != 0:
+            raise RuntimeError(f"hipEventCreateWithFlags: {rc}")
+
+    def record(self, stream):
+        rc = HipEvent._hip.hipEventRecord(self.h, ctypes.c_void_p(stream.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"hipEventRecord: {rc}")
+
+    def elapsed_time(self, end):
+        ms = ctypes.c_float()
+        rc = HipEvent._hip.hipEventElapsedTime(ctypes.byref(ms), self.h, end.h)
+        if rc != 0:
+            raise RuntimeError(f"hipEventElapsedTime: {rc}")
+        return ms.value
+
+    def __del__(self):
+        if HipEvent._hip is not None and self.h:
+            HipEvent._hip.hipEventDestroy(self.h)
 
 
 def load_pmc(path):
@@ -913,7 +949,8 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    events = [torch.cuda.Event(enable_timing=True) for _ in range(2 * args.steps + 1)]
+    events = [HipEvent() if args.events == "nofence" else torch.cuda.Event(enable_timing=True)
+              for _ in range(2 * args.steps + 1)]
     shard.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -1018,6 +1055,7 @@ def main():
         f"{two}_GiBps": round(n_total * n / (dec_ms * 1e-3) / 2**30, 3),
         "kernels": kernels,
         "roofline": roofline,
+        "timing_events": args.events,
         "settle": {"ms": round(settle_ms, 1), "steps": settle_steps,
                    "note": "untimed steps before the warmup steps, until the GPU's clocks "
                            "settle (--settle-ms)"},

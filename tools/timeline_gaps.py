@@ -3,10 +3,11 @@
 `rocprofv3 --kernel-trace [--memory-copy-trace] --output-format csv` run (dev
 tool), for slices of the dispatch sequence:
 
-    python tools/timeline_gaps.py TRACE_DIR NAME_SUBSTRING  -48:-32 -16:
+    python tools/timeline_gaps.py TRACE_DIR NAME_REGEX  -48:-32 -16:
 
 Copies (memory-copy trace) that start inside a slice's span are counted."""
 import csv
+import re
 import glob
 import os
 import statistics
@@ -24,7 +25,7 @@ def rows(trace_dir, pattern):
 def main():
     d, name = sys.argv[1], sys.argv[2]
     ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
-                for r in rows(d, "*kernel_trace.csv") if name in r["Kernel_Name"])
+                for r in rows(d, "*kernel_trace.csv") if re.search(name, r["Kernel_Name"]))
     cps = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Direction", ""))
                  for r in rows(d, "*memory_copy_trace.csv"))
     print(f"{len(ks)} dispatches of *{name}*, {len(cps)} copies")
