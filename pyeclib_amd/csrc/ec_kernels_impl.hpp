@@ -663,6 +663,10 @@ __host__ __device__ constexpr int stream_slots() {
 // vs 353.6; profiles/r03s_ab_*.txt.  The lookup latency is not what the
 // 2-per-CU launch waits on.)
 constexpr int kEncodeOcc = 8, kEncodePerCu = 2;
+// Eight-row (m = 5..8) parity encode, stream kernel: blocks per CU.  Round 5,
+// k=10 m=5 256 x 4 MiB, alternating, one box (profiles/r05s_km_sweep.txt):
+// 321.2 us at 3 against 348.3 at 2 (545.7 at 1).
+constexpr int kEncode8PerCu = 3;
 // The fused-CRC encode's register budget: 7 waves per SIMD (72 VGPRs, no
 // scratch at k = 10, m = 4) once its item range stopped feeding waterfall
 // loops (encode_crc_interior); 6 with six inputs in flight (k = 18, 24,
@@ -705,6 +709,14 @@ __device__ __forceinline__ void enc_item_pos(const EncodeParams& p, uint32_t w, 
                                              uint32_t& x) {
   o = to_sgpr(w / p.tiles);
   x = (w - o * p.tiles) * (kTile * CH) + wave_in_block() * (kChunkBytes * CH);
+}
+
+// The stream kernels skip a dropped row's store outright (a uniform branch:
+// round 5, the eight-row pass at m = 5 issued three stores per chunk into a
+// zero-record descriptor); the loader / consumer kernel keeps the dropped
+// stores, whose count its vmcnt waits assume.
+__device__ __forceinline__ bool row_live(const EncodeParams& p, int q) {
+  return q == 0 || static_cast<uint32_t>(q) < p.nrows;
 }
 
 // Parity row q's store descriptor.  A pass computes NR rows (2, 4 or 8: the
@@ -767,8 +779,8 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
   const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
 #pragma unroll
   for (int q = 0; q < NR; ++q)
-    buf_st(parity_row<NR>(p, o, q, par), t, (p.row0 + q) * p.frag_stride + kHeaderBytes,
-           zero_tail(F::row(s, q), rem));
+    if (row_live(p, q))
+      buf_st(par, t, (p.row0 + q) * p.frag_stride + kHeaderBytes, zero_tail(F::row(s, q), rem));
 }
 
 // ---------------- inline CRC-32 of the chunks a launch writes ----------------
@@ -903,7 +915,7 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
         const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x + kChunkBytes * c;
 #pragma unroll
         for (int q = 0; q < NR; ++q)
-          buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, F::row(s, q));
+          if (row_live(p, q)) buf_st(par, lane16, soff + q * p.frag_stride, F::row(s, q));
         if constexpr (CRC) {
           uint32_t* part = p.crc_part + (static_cast<uint64_t>(o) * chunks + x / kChunkBytes) * p.m + p.row0;
 #pragma unroll
@@ -2199,8 +2211,8 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     if (e != hipErrorNotSupported) return e;
   }
   if constexpr (kAB && F::kRows > kRowsPerPass) {  // eight-row encode: blocks per CU
-    const int per_cu = ab_knob("ECAMD_ENC_PER_CU", kEncodePerCu);
-    if (per_cu != kEncodePerCu && !data && p.crc_lanes == nullptr) {
+    const int per_cu = ab_knob("ECAMD_ENC_PER_CU", kEncode8PerCu);
+    if (per_cu != kEncode8PerCu && !data && p.crc_lanes == nullptr) {
       p.fused_edges = 1;
       return launch_edges_apart(encode_kernel<F, K, NR>, p, lds, p.n_obj * p.tiles, edge_items,
                                 stream, per_cu, true);
@@ -2232,7 +2244,11 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     }
   }
   if constexpr (F::kRows <= kRowsPerPass && K >= kDmaMinK) {
-    if (crc || data || (dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) &&
+    // two-row passes (m <= 2) keep the stream kernel for the plain parity
+    // encode: round 5, k=10 m=2 256 x 4 MiB, one box: 250.7 us against 309.5
+    // for the loader / consumer form (k=4 m=2: 322.3 vs 323.1;
+    // profiles/r05s_km_sweep.txt)
+    if (crc || data || (NR > 2 && dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) &&
                         !ab_knob("ECAMD_ENC_STREAM", 0))) {
       if (static_cast<uint64_t>(K) * p.bs + 65536u > 0xFFFFFFFFull) return hipErrorInvalidValue;
       e = data ? launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream, &chunks)
@@ -2249,7 +2265,7 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
       e = data ? launch_edges_apart(encode_kernel<F, K, NR, false, true>, p, lds, items, edge_items,
                                     stream, kEncodePerCu, true)
                : launch_edges_apart(encode_kernel<F, K, NR>, p, lds, items, edge_items, stream,
-                                    kEncodePerCu, true);
+                                    kEncode8PerCu, true);
     } else if constexpr (K < kDmaMinK) {
       const size_t crc_lds = crc_lds_base<F, K>() + kCrcLaneBytes;
       if (crc)

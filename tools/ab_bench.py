@@ -21,6 +21,7 @@ import argparse
 import os
 import statistics
 import sys
+import time
 
 import numpy as np
 
@@ -45,6 +46,8 @@ def main():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("variants", nargs="+")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="untimed encode + decode steps before the rounds (clock settle)")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--obj-bytes", type=int, default=4 * 1024 * 1024)
@@ -81,9 +84,14 @@ def main():
 
     import torch
     from pyeclib_amd import _native, batch
-    ab_set = _native.lib.ecamd_ab_set
-    ab_set.restype = ctypes.c_int
-    ab_set.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    if hasattr(_native.lib, "ecamd_ab_set"):
+        ab_set = _native.lib.ecamd_ab_set
+        ab_set.restype = ctypes.c_int
+        ab_set.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    elif all(v == "base" for v in args.variants):
+        ab_set = None  # the product library: only its own behaviour, no switches
+    else:
+        sys.exit(f"{args.lib} has no A/B switches: only the variant `base` runs on it")
 
     k, m, n, B = args.k, args.m, args.obj_bytes, args.batch
     dev = torch.device("cuda:0")
@@ -131,7 +139,16 @@ def main():
 
     def apply(env):
         for key in KEYS:
-            ab_set(key.encode(), int(env[key]) if key in env else -1)
+            if ab_set is not None:
+                ab_set(key.encode(), int(env[key]) if key in env else -1)
+
+    # clock settle (bench.py's --settle-ms): the first ~20 ms of load run at
+    # ramping clocks, which a short sweep's first rounds would otherwise measure
+    t_settle = time.perf_counter()
+    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+        codec.encode(objs, n, parity=stripes[:, k:], data=data)
+        second()
+        torch.cuda.synchronize()
 
     for rnd in range(args.rounds):
         for name, env in variants:
