@@ -1131,6 +1131,12 @@ def main():
     numa_all = numa
     if rank == 0:
         result["placement"] = {"rank0": numa, "cpu_affinity": len(os.sched_getaffinity(0))}
+        from pyeclib_amd import system_liberasurecode
+        result["system_liberasurecode"] = {
+            "found": system_liberasurecode.probe(),
+            "note": "ctypes.util.find_library('erasurecode') on this box (SURVEY 8(c) upgrade path); "
+                    "when found, tests/test_system_liberasurecode.py pins the oracle and the GPU "
+                    "path to its bytes"}
 
     if rank == 0 and not args.no_host and w == 16:
         result.update(host_resident(args, codec, host, stripes, masks, fs, bs))
