@@ -228,25 +228,48 @@ struct DevBuf {
 // single-object calls: the kernels read and write it over PCIe, the host
 // fills and drains it with memcpy -- no DMA copies, which from pageable
 // Python bytes cost a staged transfer each (one per fragment on decode).
+//
+// The process's instances share one budget for these buffers
+// (ECAMD_PINNED_TOTAL_MB, default 1024): a buffer that would take the total
+// past it is not grown, and that call (and the instance's later ones of that
+// size) takes the DMA path through HBM instead -- a Swift worker holding many
+// policies' instances does not pin gigabytes of host memory (round-4 advice).
+std::atomic<size_t>& pinned_total() {
+  static std::atomic<size_t> t{0};
+  return t;
+}
+size_t pinned_budget() {
+  static const size_t b = static_cast<size_t>(std::max<long>(0, env_long("ECAMD_PINNED_TOTAL_MB", 1024)))
+                          << 20;
+  return b;
+}
+
 struct PinBuf {
   uint8_t* p = nullptr;
-  size_t cap = 0;
+  size_t cap = 0;       // bytes held, counted in pinned_total()
   bool failed = false;  // allocation or mapping refused: use the DMA path
   uint8_t* ensure(size_t n) {
     if (failed) return nullptr;
     if (n <= cap) return p;
-    release();
     const size_t want = std::max<size_t>((n + (1 << 20) - 1) & ~size_t((1 << 20) - 1), 1 << 20);
+    const size_t grow = want - cap;  // the new buffer replaces the old one
+    if (pinned_total().fetch_add(grow) + grow > pinned_budget()) {
+      pinned_total().fetch_sub(grow);
+      return nullptr;  // over the budget: this call takes the DMA path
+    }
+    free_buffer();
     void* h = nullptr;
     void* d = nullptr;
     if (hipHostMalloc(&h, want, hipHostMallocMapped) != hipSuccess) {
       (void)hipGetLastError();
+      pinned_total().fetch_sub(want);
       failed = true;
       return nullptr;
     }
     if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || d != h) {
       (void)hipGetLastError();
       (void)hipHostFree(h);
+      pinned_total().fetch_sub(want);
       failed = true;
       return nullptr;
     }
@@ -255,6 +278,12 @@ struct PinBuf {
     return p;
   }
   void release() {
+    pinned_total().fetch_sub(cap);
+    free_buffer();
+  }
+
+ private:
+  void free_buffer() {  // no accounting: the caller has moved cap
     if (p) (void)hipHostFree(p);
     p = nullptr;
     cap = 0;

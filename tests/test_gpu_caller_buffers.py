@@ -152,3 +152,31 @@ def test_python_api_adjacent_bytes(oracle):
     for n in (1_150_000, 1_258_752):
         a = np.random.default_rng(n).integers(0, 256, n, dtype=np.uint8)
         assert np.array_equal(torch.from_numpy(a).to("cuda:0").cpu().numpy(), a)
+
+
+_BUDGET_CHILD = r"""
+import os, sys
+sys.path.insert(0, os.environ["ECAMD_TEST_ROOT"])
+import numpy as np
+from pyeclib_amd import ECDriver
+from oracle import oracle as O
+for n in (256 << 10, 4 << 20, 3 << 20):   # within, past, past the 1 MiB budget
+    data = np.random.Generator(np.random.PCG64(n)).integers(0, 256, n, dtype=np.uint8).tobytes()
+    d = ECDriver(k=10, m=4, ec_type="liberasurecode_rs_vand")
+    frags = d.encode(data)
+    assert frags == O.encode(10, 4, data), n
+    assert d.decode(frags[4:]) == data, n
+print("budget ok")
+"""
+
+
+def test_pinned_staging_budget():
+    """ECAMD_PINNED_TOTAL_MB caps the pinned staging all instances of a
+    process hold (round-4 advice): at 1 MiB, a 256 KiB object goes through
+    pinned staging and the 3-4 MiB ones take the DMA path, all bit-exact.  A
+    child process, so the budget (read once per process) is its own."""
+    import subprocess
+    env = dict(os.environ, ECAMD_PINNED_TOTAL_MB="1", ECAMD_TEST_ROOT=ROOT)
+    r = subprocess.run([sys.executable, "-c", _BUDGET_CHILD], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and "budget ok" in r.stdout, r.stdout + r.stderr
