@@ -255,11 +255,22 @@ struct Gf16 {
       s_hi.y = xor3(xor3(s_hi.y, e4.y, e5.y), e6.y, e7.y);
       asm volatile("" : "+v"(s_lo.x), "+v"(s_lo.y), "+v"(s_hi.x), "+v"(s_hi.y));
     } else {
-      s_lo.x = xor3(xor3(s_lo.x, lds_u32(a[0], tab + qoff(0)), lds_u32(a[1], tab + qoff(1))),
-                    lds_u32(a[2], tab + qoff(2)), lds_u32(a[3], tab + qoff(3)));
-      s_hi.x = xor3(xor3(s_hi.x, lds_u32(a[4], tab + qoff(0)), lds_u32(a[5], tab + qoff(1))),
-                    lds_u32(a[6], tab + qoff(2)), lds_u32(a[7], tab + qoff(3)));
-      asm volatile("" : "+v"(s_lo.x), "+v"(s_hi.x));
+      // Rows <= 2 use the low dword of each entry, but read the whole entry:
+      // the entries of a nibble position are 16 B apart, so ds_read_b32
+      // (banks (a/4) mod 32) puts v and v + 8 on one bank -- two-way
+      // conflicts on every lookup -- where ds_read_b64 (mod 64) is
+      // conflict-free at the same two cycles.  The high dwords feed the pin
+      // below only, so the loads are not narrowed (round 5: reconstruct, the
+      // m <= 2 decode and encode).
+      const uint2 e0 = lds_u64(a[0], tab + qoff(0)), e1 = lds_u64(a[1], tab + qoff(1)),
+                  e2 = lds_u64(a[2], tab + qoff(2)), e3 = lds_u64(a[3], tab + qoff(3));
+      const uint2 e4 = lds_u64(a[4], tab + qoff(0)), e5 = lds_u64(a[5], tab + qoff(1)),
+                  e6 = lds_u64(a[6], tab + qoff(2)), e7 = lds_u64(a[7], tab + qoff(3));
+      s_lo.x = xor3(xor3(s_lo.x, e0.x, e1.x), e2.x, e3.x);
+      s_hi.x = xor3(xor3(s_hi.x, e4.x, e5.x), e6.x, e7.x);
+      asm volatile("" : "+v"(s_lo.x), "+v"(s_hi.x)
+                   : "v"(e0.y), "v"(e1.y), "v"(e2.y), "v"(e3.y), "v"(e4.y), "v"(e5.y), "v"(e6.y),
+                     "v"(e7.y));
     }
   }
   // One symbol (h = 0: low half-word) of x at a time: half the lookup
@@ -278,10 +289,11 @@ struct Gf16 {
         s.x = xor3(xor3(s.x, e0.x, e1.x), e2.x, e3.x);
         s.y = xor3(xor3(s.y, e0.y, e1.y), e2.y, e3.y);
         asm volatile("" : "+v"(s.x), "+v"(s.y));
-      } else {
-        s.x = xor3(xor3(s.x, lds_u32(a[4 * h], tab + qoff(0)), lds_u32(a[4 * h + 1], tab + qoff(1))),
-                   lds_u32(a[4 * h + 2], tab + qoff(2)), lds_u32(a[4 * h + 3], tab + qoff(3)));
-        asm volatile("" : "+v"(s.x));
+      } else {  // whole entries, as mac_dword
+        const uint2 e0 = lds_u64(a[4 * h], tab + qoff(0)), e1 = lds_u64(a[4 * h + 1], tab + qoff(1)),
+                    e2 = lds_u64(a[4 * h + 2], tab + qoff(2)), e3 = lds_u64(a[4 * h + 3], tab + qoff(3));
+        s.x = xor3(xor3(s.x, e0.x, e1.x), e2.x, e3.x);
+        asm volatile("" : "+v"(s.x) : "v"(e0.y), "v"(e1.y), "v"(e2.y), "v"(e3.y));
       }
       lookup_fence();
     }
@@ -2418,9 +2430,17 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
         // 330.8 us against 259.9 (k=10 m=4 256 x 4 MiB) and 462.9 against
         // 447.0 (isa_l_rs_cauchy 12+4 128 x 16 MiB; tools/ab_bench.py
         // --reconstruct, profiles/r04r_ab_reconstruct.txt)
-        if (dma_batch(K, p.bs, static_cast<uint64_t>(K) * p.bs, p.n_obj, cus) &&
-            ab_knob("ECAMD_REC_DMA", 0))
+        const int rd = ab_knob("ECAMD_REC_DMA", 0);
+        if (dma_batch(K, p.bs, static_cast<uint64_t>(K) * p.bs, p.n_obj, cus) && rd != 0) {
+          if constexpr (K == 10) {  // shapes of the loader / consumer reconstruct
+            if (rd == 3) return launch_decode_dma<F, K, 3, true, 4, 12, 1, 1, kReconstruct>(p, stream);
+            if (rd == 4) return launch_decode_dma<F, K, 3, true, 4, 16, 0, 1, kReconstruct>(p, stream);
+            if (rd == 5) return launch_decode_dma<F, K, 4, true, 4, 12, 0, 1, kReconstruct>(p, stream);
+            if (rd == 6) return launch_decode_dma<F, K, 3, true, 2, 12, 0, 1, kReconstruct>(p, stream);
+            if (rd == 7) return launch_decode_dma<F, K, 3, true, 4, 8, 0, 2, kReconstruct>(p, stream);
+          }
           return launch_decode_dma<F, K, 3, true, 4, 12, 0, 1, kReconstruct>(p, stream);
+        }
       }
     }
     p.fused_edges = 1;
