@@ -162,6 +162,7 @@ void build_crc_finish_tables(uint32_t bs, bool legacy, CrcFinishTables* out) {
     meta.col[b] = apply(zeros(59 - 25, legacy), r);
   }
   nibble_tables(meta, out->meta);
+  for (int k = 0; k < 6; ++k) nibble_tables(zeros(uint64_t(16) << k, legacy), out->z16[k]);
   out->init_term = apply(zeros(bs, legacy), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
 }
 

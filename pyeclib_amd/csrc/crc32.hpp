@@ -53,6 +53,7 @@ struct CrcFinishTables {
   uint32_t pow[kCrcPowBits][8][16];  // Z_{1024 * 2^i}
   uint32_t zr[8][16];                // Z_{bs mod 1024}
   uint32_t meta[8][16];              // c (header bytes 21..24) -> metadata checksum change
+  uint32_t z16[6][8][16];            // Z_{16 * 2^k}: the lane tree of an edge chunk
   uint32_t init_term;                // Z_bs(0xFFFFFFFF) ^ 0xFFFFFFFF
   uint32_t pad[3];
 };

@@ -1,5 +1,6 @@
 // Host restatement of the GPU inline-CRC scheme (crc_device.hpp chunk_crc,
-// ec_crc.hip crc_finish_kernel), checked against the byte-serial CRCs.
+// ec_crc.hip crc_finish_kernel -- finish_tree, round 5; finish, the round-4
+// form), checked against the byte-serial CRCs.
 // Built and run by tests/test_crc_math.py with g++ against
 // pyeclib_amd/csrc/crc32.cpp -- no GPU, no HIP.
 //
@@ -72,6 +73,62 @@ static uint32_t finish(const CrcLaneTables& L, const CrcFinishTables& F, const u
   return zmap(F.zr, acc) ^ edge ^ F.init_term;
 }
 
+// 64 lanes' values joined by the level maps tab(k) (ec_crc.hip lane_tree;
+// lanes below 2^k take their own value, as __shfl_up gives them)
+template <class Tab>
+static uint32_t lane_tree(std::vector<uint32_t> v, Tab tab) {
+  for (int k = 0; k < 6; ++k) {
+    std::vector<uint32_t> n(64);
+    for (int l = 0; l < 64; ++l) n[l] = zmap(tab(k), v[l >= (1 << k) ? l - (1 << k) : l]) ^ v[l];
+    v = n;
+  }
+  return v[63];
+}
+
+// the round-5 finishing pass: runs of L chunks per thread (Horner by
+// Z_1024), the lane tree by Z_{1024 L 2^k}, the waves by Z_{1024 64 L}, the
+// shift from chunk n's end to nfull's; edge chunks by the Z_{16 2^k} tree
+static uint32_t finish_tree(const CrcLaneTables& L, const CrcFinishTables& F, const uint8_t* pay,
+                            uint32_t bs, uint32_t n) {
+  const uint32_t nfull = bs / 1024;
+  uint32_t lg = 0;
+  while ((256u << lg) < n) ++lg;
+  const uint32_t run = 1u << lg;
+  const int64_t lead = int64_t(256u << lg) - n;
+  uint32_t red[4];
+  for (int w = 0; w < 4; ++w) {
+    std::vector<uint32_t> v(64);
+    for (int l = 0; l < 64; ++l) {
+      uint32_t acc = 0;
+      for (uint32_t j = 0; j < run; ++j) {
+        const int64_t c = int64_t(64 * w + l) * run + j - lead;
+        const uint32_t x = c >= 0 ? chunk_crc(L, pay + 1024 * c) : 0u;
+        acc = (j == 0 ? 0u : zmap(F.pow[0], acc)) ^ x;
+      }
+      v[l] = acc;
+    }
+    red[w] = lane_tree(v, [&](int k) { return F.pow[lg + k]; });
+  }
+  uint32_t a = red[0];
+  for (int w = 1; w < 4; ++w) a = zmap(F.pow[lg + 6], a) ^ red[w];
+  a = shift_chunks(F, a, nfull - n);
+  const int64_t e0 = int64_t(n) * 1024;
+  const uint32_t n_edge = static_cast<uint32_t>((int64_t(bs) - e0 + 1023) / 1024);
+  uint32_t edge = 0;
+  for (uint32_t j = 0; j < n_edge; ++j) {
+    uint8_t buf[1024];
+    const int64_t start = int64_t(bs) - 1024 * int64_t(j + 1);
+    for (int b = 0; b < 1024; ++b) {
+      const int64_t at = start + b;
+      buf[b] = (at >= e0 && at < int64_t(bs)) ? pay[at] : 0;
+    }
+    std::vector<uint32_t> v(64);
+    for (int l = 0; l < 64; ++l) v[l] = raw16(L, buf + 16 * l);
+    edge ^= shift_chunks(F, lane_tree(v, [&](int k) { return F.z16[k]; }), j);
+  }
+  return zmap(F.zr, a) ^ edge ^ F.init_term;
+}
+
 int main() {
   std::mt19937_64 rng(20261018);
   int failures = 0, checks = 0;
@@ -94,6 +151,12 @@ int main() {
         if (got != want) {
           ++failures;
           std::printf("FAIL legacy=%d bs=%u chunks=%u got %08x want %08x\n", legacy, bs, chunks, got, want);
+        }
+        ++checks;
+        const uint32_t got2 = finish_tree(*L, *F, pay.data(), bs, chunks);
+        if (got2 != want) {
+          ++failures;
+          std::printf("FAIL tree legacy=%d bs=%u chunks=%u got %08x want %08x\n", legacy, bs, chunks, got2, want);
         }
       }
       // metadata checksum: delta from chksum[0] = 0 to chksum[0] = want
