@@ -176,6 +176,20 @@ int ecamd_encode_into(int desc, const char *data, uint64_t data_len, char **frag
  * out, [5] headers.  Returns the count written (<= n) or -errno. */
 int ecamd_call_phases(int desc, double *us, int n);
 
+/* Bookkeeping of an instance, for tests: [0] stream end marks held (a
+ * caller that takes a new stream per call must not grow it), [1] pinned
+ * staging bytes held by the process, [2] single-object calls of this
+ * instance that staged through HBM instead (over the pinned budget or past
+ * the size limit), [3] the process's pinned budget in bytes
+ * (ECAMD_PINNED_TOTAL_MB).  Returns the count written (<= n) or -errno. */
+int ecamd_instance_stats(int desc, uint64_t *out, int n);
+
+/* The device-runtime error behind the calling thread's last -EBACKENDINITERR
+ * from an entry point (pyeclib maps that code to "Unknown error",
+ * pyeclib_c.c:170-173): its name and text into buf (NUL-terminated, at most
+ * n bytes); returns the runtime's error code, 0 when the last call had none. */
+int ecamd_last_device_error(char *buf, uint64_t n);
+
 /* liberasurecode_decode (pyeclib_c.c:878) into a caller buffer of exactly
  * the decoded length (orig_data_size of the fragments' headers; else
  * -EINVALIDPARAMS).  Same checks, fast path and errors; synchronous. */

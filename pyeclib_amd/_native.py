@@ -183,6 +183,8 @@ _sig.update({
     "ecamd_decode_into": (ctypes.c_int, [ctypes.c_int, _cpp, ctypes.c_int, ctypes.c_uint64,
                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64]),
     "ecamd_call_phases": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_double), ctypes.c_int]),
+    "ecamd_last_device_error": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64]),
+    "ecamd_instance_stats": (ctypes.c_int, [ctypes.c_int, _P(ctypes.c_uint64), ctypes.c_int]),
 })
 EXPORTS = tuple(_sig)
 for _name, (_res, _args) in _sig.items():
@@ -219,8 +221,33 @@ def _exception_class(name: str) -> type:
     return getattr(_local_exc, name)
 
 
+def last_device_error() -> tuple[int, str]:
+    """The device-runtime error behind this thread's last -EBACKENDINITERR
+    (ecamd_last_device_error): (code, "name: text"), code 0 when none."""
+    buf = ctypes.create_string_buffer(256)
+    code = int(lib.ecamd_last_device_error(buf, len(buf)))
+    return code, buf.value.decode(errors="replace")
+
+
+def instance_stats(handle: "PyECLibHandle") -> dict:
+    """ecamd_instance_stats: the instance's stream marks, the process's
+    pinned staging bytes and budget, and its single-object calls that staged
+    through HBM (tests)."""
+    out = (ctypes.c_uint64 * 4)()
+    ret = lib.ecamd_instance_stats(handle.desc, out, 4)
+    if ret < 0:
+        raise_error(ret, "ecamd_instance_stats")
+    return {"marks": out[0], "pinned_bytes": out[1], "dma_calls": out[2], "pinned_budget": out[3]}
+
+
 def raise_error(ret: int, prefix: str) -> None:
     name, msg = _ERRORS.get(ret, ("ECDriverError", "Unknown error"))
+    if ret == -EBACKENDINITERR:
+        # pyeclib says "Unknown error" here (pyeclib_c.c:170-173); a device
+        # fault behind it is named, so the cause is not lost in the mapping
+        code, text = last_device_error()
+        if code:
+            msg = f"{msg} (device: {text})"
     cls = _exception_class(name)
     raise cls(f"{prefix} ERROR: {msg}. Please inspect syslog for liberasurecode error report.")
 

@@ -723,6 +723,19 @@ __device__ __forceinline__ void enc_item_pos(const EncodeParams& p, uint32_t w, 
   x = (w - o * p.tiles) * (kTile * CH) + wave_in_block() * (kChunkBytes * CH);
 }
 
+// Store descriptors of object o's parity and data fragments, clipped to
+// those fragments' bytes (m or k fragment strides; below 4 GiB by
+// layout_fits), so the range check drops any store that would leave them
+// (round 6; until then they held 4 GiB - 1 records).
+__device__ __forceinline__ Rsrc rsrc_parity(const EncodeParams& p, uint32_t o) {
+  return rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride,
+              static_cast<int>(p.m * static_cast<uint32_t>(p.frag_stride)));
+}
+__device__ __forceinline__ Rsrc rsrc_data(const EncodeParams& p, uint32_t o) {
+  return rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride,
+              static_cast<int>(p.k * static_cast<uint32_t>(p.frag_stride)));
+}
+
 // The stream kernels skip a dropped row's store outright (a uniform branch:
 // round 5, the eight-row pass at m = 5 issued three stores per chunk into a
 // zero-record descriptor); the loader / consumer kernel keeps the dropped
@@ -762,7 +775,7 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
   typename F::Acc s;
   F::zero(s);
   Rsrc dat;
-  if constexpr (DATA) dat = rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride);
+  if constexpr (DATA) dat = rsrc_data(p, o);
 #pragma unroll
   for (int j0 = 0; j0 < K; j0 += kEdgeGroup) {
     constexpr int G = kEdgeGroup;
@@ -788,7 +801,7 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
   // the payload's last unit is stored whole with its bytes past bs zeroed
   // (slot padding): no byte loop (store_partial's, inlined here, put up to
   // 1.4 KB per lane of scratch in the small-k kernels)
-  const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
+  const Rsrc par = rsrc_parity(p, o);
 #pragma unroll
   for (int q = 0; q < NR; ++q)
     if (row_live(p, q))
@@ -892,8 +905,8 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
     enc_item_pos<CH>(p, wn, on, xn);
     const Rsrc nxt = rsrc(p.objs + static_cast<uint64_t>(on) * p.obj_stride, wn == w ? 0 : -1);
     Rsrc dat;
-    if constexpr (DATA) dat = rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride);
-    const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
+    if constexpr (DATA) dat = rsrc_data(p, o);
+    const Rsrc par = rsrc_parity(p, o);
     typename F::Acc s;
     F::zero(s);
 #pragma unroll
@@ -1207,9 +1220,9 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   for (uint32_t i = 0; i < n_items; ++i) {
     uint32_t o, x0;
     item_at(i, o, x0);
-    const Rsrc par = rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride);
+    const Rsrc par = rsrc_parity(p, o);
     Rsrc dat;
-    if constexpr (DATA) dat = rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride);
+    if constexpr (DATA) dat = rsrc_data(p, o);
 #pragma unroll
     for (int j = 0; j < K; ++j) {
       // (vmcnt counts the data-fragment stores too: the wait is then
@@ -1439,6 +1452,51 @@ __device__ __forceinline__ DescU load_desc(const DecodeParams& p, uint32_t o) {
   return u;
 }
 
+// Debug builds (`make -C pyeclib_amd/csrc checks`, -DECAMD_DEVICE_CHECKS):
+// every descriptor is checked before a store that depends on it, and the
+// edge items' flat stores against their slice; a violation prints what it
+// found (lane 0) and traps, so the launch fails with an error instead of
+// writing where a bad index points.  The product build compiles none of it.
+#ifdef ECAMD_DEVICE_CHECKS
+#define ECAMD_DEVICE_ASSERT(cond, ...)               \
+  do {                                               \
+    if (!(cond)) {                                   \
+      if (lane_id() == 0) printf(__VA_ARGS__);       \
+      __builtin_trap();                              \
+    }                                                \
+  } while (0)
+#else
+#define ECAMD_DEVICE_ASSERT(cond, ...) \
+  do {                                 \
+  } while (0)
+#endif
+
+// Object o's descriptor: inputs are fragment indices < k + m; rows per pass
+// at most 8; decode rows rebuild data indices < k, a reconstruct row any
+// fragment index.
+template <int K, int MODE>
+__device__ __forceinline__ void check_desc(const DecodeParams& p, const DescU& d, uint32_t o) {
+#ifdef ECAMD_DEVICE_CHECKS
+  const uint32_t n = p.k + p.m;
+  ECAMD_DEVICE_ASSERT(o < p.n_obj && p.k == static_cast<uint32_t>(K),
+                      "ecamd check: object %u of %u, k %u (kernel K %d)\n", o, p.n_obj, p.k, K);
+#pragma unroll
+  for (int c = 0; c < K; ++c)
+    ECAMD_DEVICE_ASSERT(d.in_idx(c) < n, "ecamd check: object %u input %d index %u >= %u\n", o, c,
+                        d.in_idx(c), n);
+  ECAMD_DEVICE_ASSERT(d.n_out() <= 4u, "ecamd check: object %u rows %u\n", o, d.n_out());
+  const uint32_t lim = MODE == kReconstruct ? n : static_cast<uint32_t>(K);
+#pragma unroll
+  for (uint32_t q = 0; q < 4; ++q)
+    ECAMD_DEVICE_ASSERT(q >= d.n_out() || d.out_idx(q) < lim,
+                        "ecamd check: object %u row %u index %u >= %u\n", o, q, d.out_idx(q), lim);
+#else
+  (void)p;
+  (void)d;
+  (void)o;
+#endif
+}
+
 // Fragment group position of input c.
 __device__ __forceinline__ uint32_t in_pos(const DecodeParams& p, const DescU& d, int c) {
   return p.compact ? static_cast<uint32_t>(c) : d.in_idx(c);
@@ -1450,15 +1508,29 @@ __device__ __forceinline__ void dec_item_pos(const DecodeParams& p, uint32_t w, 
   x = (w - o * p.tiles) * kTile + wave_in_block() * kChunkBytes;
 }
 
-// Output descriptor: 2 GiB - 1 records, so a voffset of kDrop (2 GiB) makes
-// the buffer range check discard that lane's store.
+// Output descriptor of one object (decode: its obj_len bytes) or one
+// fragment (reconstruct: 80 + bs bytes), so the hardware range check clips
+// any store that would leave the destination (round 6; until then every
+// output descriptor held 2 GiB - 1 records).  Every extent is below 2 GiB
+// (layout_fits), so a store sent to voffset kDrop (2 GiB) with soffset 0 is
+// always discarded: drop_st never adds a per-input soffset to kDrop, whose
+// sum could wrap past 2^32 back into the destination.
 constexpr uint32_t kDrop = 0x80000000u;
-__device__ __forceinline__ Rsrc rsrc_out(const void* base) {
+template <int MODE>
+__device__ __forceinline__ uint32_t out_extent(const DecodeParams& p) {
+  return MODE == kReconstruct ? kHeaderBytes + p.bs : static_cast<uint32_t>(p.obj_len);
+}
+__device__ __forceinline__ Rsrc rsrc_out(const void* base, uint32_t records) {
   const uint64_t a = reinterpret_cast<uint64_t>(base);
   const uint32_t lo = to_sgpr(static_cast<uint32_t>(a));
   const uint32_t hi = to_sgpr(static_cast<uint32_t>(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo), 0, 0x7FFFFFFF, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>((static_cast<uint64_t>(hi) << 32) | lo),
+                                           0, static_cast<int>(to_sgpr(records)), 0x00020000);
+}
+// A store that applies only when `live` (wave-uniform): otherwise it goes to
+// kDrop with soffset 0 and the range check discards it.
+__device__ __forceinline__ void drop_st(Rsrc r, bool live, uint32_t lane16, uint32_t soff, const uint4& v) {
+  buf_st(r, live ? lane16 : kDrop, live ? soff : 0u, v);
 }
 
 // Interior decode / reconstruct, streaming the first k available fragments.
@@ -1534,8 +1606,9 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
     const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
     table_prefetch<F, K>(p, dn.table(), wn != w && dn.n_out() != 0 && dn.table() != st.table,
                          pre);
-    const Rsrc out = rsrc_out(p.out + static_cast<uint64_t>(o) * p.out_stride);
+    const Rsrc out = rsrc_out(p.out + static_cast<uint64_t>(o) * p.out_stride, out_extent<MODE>(p));
     const bool copy = MODE != kReconstruct && d.copy_inputs() != 0;
+    check_desc<K, MODE>(p, d, o);
     typename F::Acc s;
     F::zero(s);
 #pragma unroll
@@ -1548,8 +1621,8 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
           F::mac(kb, j * F::kTableBytes, buf[j % NB], s);
         }
         if constexpr (MODE != kReconstruct)
-          buf_st(out, copy && d.in_idx(j) < static_cast<uint32_t>(K) ? lane16 : kDrop,
-                 d.in_idx(j) * p.bs + x, buf[j % NB]);
+          drop_st(out, copy && d.in_idx(j) < static_cast<uint32_t>(K), lane16, d.in_idx(j) * p.bs + x,
+                  buf[j % NB]);
       }
       if (j + NB < KP) {
         if (j + NB < K)
@@ -1570,8 +1643,7 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
       const uint32_t e = d.n_out();
 #pragma unroll
       for (int q = 0; q < F::kRows; ++q)
-        buf_st(out, q < static_cast<int>(e) ? lane16 : kDrop, d.out_idx(q) * p.bs + x,
-               F::row(s, q));
+        drop_st(out, q < static_cast<int>(e), lane16, d.out_idx(q) * p.bs + x, F::row(s, q));
     }
     if (wn == w) break;
     w = wn;
@@ -1590,9 +1662,14 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
   const uint32_t o = e / p.edge_tiles;
   const uint32_t tail0 = p.tiles * p.tile_ch * kTile;
   const DescU d = load_desc(p, o);
+  check_desc<K, MODE>(p, d, o);
   const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
   const uint32_t t = tail0 + (e - o * p.edge_tiles) * kTile + threadIdx.x * 16;
   if (t >= p.bs) return;
+  // the flat stores below stay inside the object (decode: slice idx < K,
+  // window ends at object_bytes) or the payload (reconstruct)
+  ECAMD_DEVICE_ASSERT(MODE == kReconstruct || static_cast<uint64_t>(K - 1) * p.bs < p.obj_len + p.bs,
+                      "ecamd check: object %u: k * bs %u short of obj_len\n", o, p.bs);
   uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
   // t < bs and 16 | t, so t + 16 <= round16(bs) <= frag_stride - 80: in bounds
   const uint8_t* in = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
@@ -1808,8 +1885,9 @@ __global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
   for (uint32_t i = 0; i < n_items; ++i) {
     uint32_t o, x0;
     item_at(i, o, x0);
-    const Rsrc out = rsrc_out(p.out + static_cast<uint64_t>(o) * p.out_stride);
+    const Rsrc out = rsrc_out(p.out + static_cast<uint64_t>(o) * p.out_stride, out_extent<MODE>(p));
     const bool copy = MODE != kReconstruct && d.copy_inputs() != 0;
+    check_desc<K, MODE>(p, d, o);
     // the slot of item i + 1's set (the one item i - 1 used, or this one again)
     const bool swap = i + 1 < n_items && dn.n_out() != 0 && dn.table() != table;
     const uint32_t kb = F::kb(slot * kTab);
@@ -1842,8 +1920,7 @@ __global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
       }
       if constexpr (MODE != kReconstruct) {
         const uint32_t slice = PROBE == 2 ? (d.in_idx(j) * p.bs) & ~15u : d.in_idx(j) * p.bs;
-        buf_st(out, copy && d.in_idx(j) < static_cast<uint32_t>(K) ? lane16 : kDrop,
-               slice + x0 + wave * 1024, xv);
+        drop_st(out, copy && d.in_idx(j) < static_cast<uint32_t>(K), lane16, slice + x0 + wave * 1024, xv);
       }
       ring = ring + 1 == R ? 0 : ring + 1;
     }
@@ -1855,7 +1932,7 @@ __global__ void __launch_bounds__(W * 64) decode_dma_kernel(DecodeParams p) {
 #pragma unroll
       for (int q = 0; q < F::kRows; ++q) {
         const uint32_t slice = PROBE == 2 ? (d.out_idx(q) * p.bs) & ~15u : d.out_idx(q) * p.bs;
-        buf_st(out, q < static_cast<int>(e) ? lane16 : kDrop, slice + x0 + wave * 1024, F::row(s, q));
+        drop_st(out, q < static_cast<int>(e), lane16, slice + x0 + wave * 1024, F::row(s, q));
       }
     }
     if (swap) {

@@ -17,6 +17,7 @@
 #include <atomic>
 #include <chrono>
 #include <cerrno>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -191,7 +192,15 @@ bool header_invalid(const uint8_t* h) {
          stored != crc32_legacy(0, h, sizeof(fragment_metadata_t));
 }
 
-int hip_errno(hipError_t e) { return e == hipErrorOutOfMemory ? -ENOMEM : -EBACKENDINITERR; }
+// The HIP error behind the calling thread's last -EBACKENDINITERR (pyeclib
+// reports it as "Unknown error"; ecamd_last_device_error hands the runtime's
+// name and text to the binding, which appends them to the message).  Reset
+// by every entry point that may launch (CallScope).
+thread_local hipError_t t_last_hip = hipSuccess;
+int hip_errno(hipError_t e) {
+  t_last_hip = e;
+  return e == hipErrorOutOfMemory ? -ENOMEM : -EBACKENDINITERR;
+}
 
 struct DeviceGuard {
   int prev = -1;
@@ -253,10 +262,12 @@ struct PinBuf {
     if (n <= cap) return p;
     const size_t want = std::max<size_t>((n + (1 << 20) - 1) & ~size_t((1 << 20) - 1), 1 << 20);
     const size_t grow = want - cap;  // the new buffer replaces the old one
-    if (pinned_total().fetch_add(grow) + grow > pinned_budget()) {
-      pinned_total().fetch_sub(grow);
-      return nullptr;  // over the budget: this call takes the DMA path
-    }
+    // reserve `grow` only if the total stays within the budget (a CAS loop:
+    // the process total never passes it, even for an instant)
+    size_t cur = pinned_total().load();
+    do {
+      if (cur + grow > pinned_budget()) return nullptr;  // over budget: the DMA path
+    } while (!pinned_total().compare_exchange_weak(cur, cur + grow));
     free_buffer();
     void* h = nullptr;
     void* d = nullptr;
@@ -361,8 +372,10 @@ struct Instance {
   //     then on every call records its end mark on its stream (CallScope).
   //   * The instance's own streams are valid while it lives: marked lazily,
   //     when something must wait for them.
-  // Entries whose recorded work has completed are dropped, so a caller
-  // taking a new stream per call does not grow the list.
+  // Entries whose recorded work has completed are dropped -- whenever a
+  // new stream would take the list past kMarkPrune entries, and before
+  // every GPU-side ordering -- so a caller taking a new stream per call
+  // holds at most about kMarkPrune plus its in-flight calls.
   struct StreamMark {
     hipStream_t s;
     hipEvent_t ev;
@@ -371,6 +384,7 @@ struct Instance {
     bool recorded;  // ev marks the end of this instance's work on s
   };
   std::vector<StreamMark> marks;
+  static constexpr size_t kMarkPrune = 16;
   bool multi = false;  // has seen two caller streams: caller calls are marked
   DevBuf enc_tables;  // passes x k x 64 u64
   // GF(2^16) with 4 < m <= 8: one eight-row table set (k x 1 KiB), so encode
@@ -401,6 +415,7 @@ struct Instance {
   double phase_us[6] = {0, 0, 0, 0, 0, 0};
   DevBuf scratch;  // single-object staging
   PinBuf pin;      // single-object staging, zero-copy (small objects)
+  uint64_t dma_calls = 0;  // single-object calls that staged through HBM (ecamd_instance_stats)
   RingSlot ring[kRing];
   int ring_pos = 0;
   UploadCache dec_cache, rec_cache, hdr_cache;
@@ -473,6 +488,9 @@ struct Instance {
     const hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e != hipSuccess) return e;
     marks.push_back({s, ev, own, true, false});
+    // a caller taking a new stream per call adds one entry per call: drop
+    // the completed ones once the list passes a few (round-5 advice)
+    if (marks.size() > kMarkPrune) prune_marks(s);
     return hipSuccess;
   }
   // End of a call: mark the end of its work on every caller stream it
@@ -647,7 +665,7 @@ struct Instance {
 // call's end marks are recorded however it returns (Instance::end_call).
 struct CallScope {
   Instance& I;
-  explicit CallScope(Instance& i) : I(i) {}
+  explicit CallScope(Instance& i) : I(i) { t_last_hip = hipSuccess; }
   CallScope(const CallScope&) = delete;
   CallScope& operator=(const CallScope&) = delete;
   ~CallScope() { (void)I.end_call(); }
@@ -1767,6 +1785,7 @@ int encode_into(Instance& I, const char* data, uint64_t len, uint8_t* const* fra
     const bool direct = I.knobs.register_caller && src.pin(data, obj_bytes);
     const uint64_t staged = direct ? 0 : obj_bytes;
     uint8_t* pin = len <= I.knobs.single_pinned_max ? I.pin.ensure(staged + fs * m) : nullptr;
+    I.dma_calls += pin == nullptr;
     hipError_t e = hipSuccess;
     if (!pin && (e = I.scratch.ensure(staged + fs * m)) != hipSuccess) return hip_errno(e);
     uint8_t* base = pin ? pin : I.scratch.b();
@@ -2009,6 +2028,7 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
   const bool direct = I.knobs.register_caller && dst.pin(out, orig);
   const size_t need = fs * (k + I.m) + (direct ? 0 : obj_bytes);
   uint8_t* pin = orig <= I.knobs.single_pinned_max ? I.pin.ensure(need) : nullptr;
+  I.dma_calls += pin == nullptr;
   hipError_t e = hipSuccess;
   if (!pin && (e = I.scratch.ensure(need)) != hipSuccess) return hip_errno(e);
   uint8_t* d_frags = pin ? pin : I.scratch.b();
@@ -2119,6 +2139,7 @@ int liberasurecode_reconstruct_fragment(int desc, char** available_fragments, in
     const uint64_t fs = round16(kHeaderBytes + round16(bs));
     const size_t need = fs * (k + m + 1);
     uint8_t* pin = orig <= I->knobs.single_pinned_max ? I->pin.ensure(need) : nullptr;
+    I->dma_calls += pin == nullptr;
     hipError_t e = hipSuccess;
     if (!pin && (e = I->scratch.ensure(need)) != hipSuccess) return hip_errno(e);
     uint8_t* d_frags = pin ? pin : I->scratch.b();
@@ -2218,6 +2239,23 @@ int ecamd_call_phases(int desc, double* us, int n) {
   const int c = std::min(n, 6);
   for (int i = 0; i < c; ++i) us[i] = I->phase_us[i];
   return c;
+}
+
+int ecamd_instance_stats(int desc, uint64_t* out, int n) {
+  auto I = lookup(desc);
+  if (!I) return -EBACKENDNOTAVAIL;
+  if (!out || n < 0) return -EINVALIDPARAMS;
+  std::lock_guard<std::mutex> lk(I->mu);
+  const uint64_t v[4] = {I->marks.size(), pinned_total().load(), I->dma_calls, pinned_budget()};
+  const int c = std::min(n, 4);
+  for (int i = 0; i < c; ++i) out[i] = v[i];
+  return c;
+}
+
+int ecamd_last_device_error(char* buf, uint64_t n) {
+  const hipError_t e = t_last_hip;
+  if (buf && n) std::snprintf(buf, n, "%s: %s", hipGetErrorName(e), hipGetErrorString(e));
+  return static_cast<int>(e);
 }
 
 int ecamd_encode_into(int desc, const char* data, uint64_t data_len, char** fragments,

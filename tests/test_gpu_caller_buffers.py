@@ -169,7 +169,9 @@ for n in (256 << 10, 4 << 20, 3 << 20):
 # several instances from several threads against one small budget: some
 # calls pinned, some on the DMA path, every output exact
 import threading
+from pyeclib_amd import _native
 errs = []
+stats = []
 def worker(t):
     try:
         d = ECDriver(k=10, m=4, ec_type="liberasurecode_rs_vand")
@@ -180,21 +182,29 @@ def worker(t):
             frags = d.encode(data)
             assert frags == O.encode(10, 4, data), (t, i)
             assert d.decode(frags[3:]) == data, (t, i)
+            stats.append(_native.instance_stats(d.ec_lib_reference._handle))
     except Exception as e:  # noqa: BLE001
         errs.append(repr(e))
 ts = [threading.Thread(target=worker, args=(t,)) for t in range(6)]
 for t in ts: t.start()
 for t in ts: t.join()
 assert not errs, errs
+# the budget held: never more than 8 MiB pinned, and some calls staged
+# through HBM because of it
+assert stats and all(s["pinned_budget"] == 8 << 20 for s in stats), stats[:1]
+assert max(s["pinned_bytes"] for s in stats) <= 8 << 20, max(s["pinned_bytes"] for s in stats)
+assert sum(s["dma_calls"] for s in stats) > 0, stats
 print("budget ok")
 """
 
 
 def test_pinned_staging_budget():
     """ECAMD_PINNED_TOTAL_MB caps the pinned staging all instances of a
-    process hold (round-4 advice): at 1 MiB, a 256 KiB object goes through
-    pinned staging and the 3-4 MiB ones take the DMA path, all bit-exact.  A
-    child process, so the budget (read once per process) is its own."""
+    process hold (round-4 advice): at 8 MiB, six instances on six threads
+    with 1-4 MiB objects share it -- the process never holds more than 8 MiB
+    pinned (ecamd_instance_stats), some calls take the DMA path through HBM
+    instead, and every output is bit-exact.  A child process, so the budget
+    (read once per process) is its own."""
     import subprocess
     env = dict(os.environ, ECAMD_PINNED_TOTAL_MB="8", ECAMD_TEST_ROOT=ROOT)
     r = subprocess.run([sys.executable, "-c", _BUDGET_CHILD], env=env, capture_output=True,

@@ -213,3 +213,41 @@ def test_destroyed_caller_streams(gpu, oracle, monkeypatch):
         assert hip.hipStreamSynchronize(s) == 0
         assert hip.hipStreamDestroy(s) == 0
         assert torch.equal(out[:, :n].cpu(), torch.from_numpy(host[:, :n])), call
+
+
+def test_stream_marks_stay_bounded(gpu, oracle):
+    """Round-5 advice: an encode-only caller that takes a new stream per call
+    (header cache resident, no pool recycle) once grew the instance's stream
+    end marks by one event per call.  300 encodes, each on a stream created
+    and destroyed around the call: the marks stay bounded
+    (ecamd_instance_stats) and every parity row matches the oracle's."""
+    import ctypes
+    import torch
+    from pyeclib_amd import _native, batch
+    import importlib.util
+    lib = os.path.join(importlib.util.find_spec("torch").submodule_search_locations[0], "lib",
+                       "libamdhip64.so")
+    hip = ctypes.CDLL(lib if os.path.exists(lib) else "libamdhip64.so")
+    hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    k, m, n, B = 10, 4, (64 << 10) + 10, 4
+    codec = batch.BatchCodec(k, m)
+    host = _objects(B, n, 9)
+    objs = torch.from_numpy(host).to(gpu)
+    stripes = batch.stripe_buffer(B, k, m, codec.blocksize(n), device=gpu)
+    torch.cuda.synchronize()
+    peak = 0
+    for call in range(300):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        codec.encode(objs, n, parity=stripes[:, k:], stream=s.value)
+        assert hip.hipStreamSynchronize(s) == 0
+        assert hip.hipStreamDestroy(s) == 0
+        peak = max(peak, _native.instance_stats(codec.handle)["marks"])
+    assert peak <= 20, peak
+    want = oracle.encode(k, m, host[0, :n].tobytes())
+    got = stripes[0].cpu().numpy()
+    fl = 80 + codec.blocksize(n)
+    for i in range(k, k + m):
+        assert got[i, :fl].tobytes() == want[i], i

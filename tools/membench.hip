@@ -551,6 +551,136 @@ __global__ void __launch_bounds__(256) dec_kernel(Shape s) {
   }
 }
 
+// ---- the guide's ceilings (MI355X_MICROARCH.md, chip table: "6.29 TB/s
+// measured (float4 copy)"; price table row ldsdma-fill: an LDS-DMA stream
+// "chip 6.4 TB/s default policy, 6.5-6.8 nt"), rebuilt here so they run on
+// the same box, in the same call, as the product kernels (round 6). ----
+
+// One float4 per thread and U per block-stride, no loop: the textbook copy.
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) copy_f4_kernel(const uint8_t* src, uint8_t* dst, uint64_t n16) {
+  const uint64_t base = uint64_t(blockIdx.x) * 256 * U + threadIdx.x;
+  v4u v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (base + u * 256 < n16) v[u] = ld<NT>(src + (base + u * 256) * 16);
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (base + u * 256 < n16) st<NT>(dst + (base + u * 256) * 16, v[u]);
+}
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) read_f4_kernel(const uint8_t* src, uint64_t n16, uint32_t* sink) {
+  const uint64_t base = uint64_t(blockIdx.x) * 256 * U + threadIdx.x;
+  uint32_t acc = 0;
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (base + u * 256 < n16) {
+      const v4u v = ld<NT>(src + (base + u * 256) * 16);
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// LDS-DMA (buffer_load_dwordx4 ... lds) as the product issues it
+// (ec_kernels_impl.hpp dma16): M0 = the wave's LDS destination, 1 KiB per
+// wave-instruction.
+typedef unsigned int v4u_s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4u_s rsrc4(const void* base, uint32_t records) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  v4u_s r;
+  r.x = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  r.y = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32)) & 0xFFFFu;
+  r.z = __builtin_amdgcn_readfirstlane(records);
+  r.w = 0x00020000u;
+  return r;
+}
+template <bool NT>
+__device__ __forceinline__ void dma16(v4u_s r, uint32_t voff, uint32_t soff, uint32_t lds) {
+  uint32_t keep;
+  if constexpr (NT)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep) : "v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Read-only LDS-DMA stream (the guide's ldsdma-fill row): L loader waves per
+// block, no consumers; each wave keeps D 1-KiB DMAs in flight into a ring of
+// D slots of its own.  Chunk c of wave (b, w) = b * L + w + i * grid * L.
+template <int L, int D, bool NT>
+__global__ void __launch_bounds__(L * 64) dma_read_kernel(const uint8_t* src, uint64_t n) {
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane16 = (threadIdx.x & 63) * 16;
+  const v4u_s r = rsrc4(src, 0xFFFFFFFFu);
+  const uint64_t chunks = n / 1024, stride = uint64_t(gridDim.x) * L;
+  uint32_t slot = 0;
+  for (uint64_t c = uint64_t(blockIdx.x) * L + wave; c < chunks; c += stride) {
+    dma16<NT>(r, lane16, __builtin_amdgcn_readfirstlane(uint32_t(c * 1024)), (wave * D + slot) * 1024);
+    slot = slot + 1 == D ? 0 : slot + 1;
+    wait_vm<D - 1>();
+  }
+  wait_vm<0>();
+}
+
+// Copy through an LDS-DMA ring, the product's loader / consumer shape
+// (decode_dma_kernel without the lookups): W waves per block, L of them
+// loaders, R ring slots of W KiB; every wave reads its 1 KiB of the slot and
+// stores it (nt) to dst.  Item = W KiB; one block per CU walks the items
+// grid-stride.
+template <int W, int L, int R, bool NT>
+__global__ void __launch_bounds__(W * 64) dma_copy_kernel(const uint8_t* src, uint8_t* dst, uint64_t n) {
+  constexpr uint32_t kSlot = 1024u * W;
+  constexpr int kPer = W / L;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane16 = (threadIdx.x & 63) * 16;
+  const bool loader = wave < uint32_t(L);
+  const uint32_t items = uint32_t(n / kSlot);
+  const uint32_t n_items = blockIdx.x < items ? (items - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+  if (n_items == 0) return;
+  auto issue = [&](uint32_t i, uint32_t ri) {
+    if (!loader) return;
+    const uint32_t it = blockIdx.x + (i < n_items ? i : 0) * gridDim.x;
+    const v4u_s r = rsrc4(src, i < n_items ? 0xFFFFFFFFu : 0u);
+    const uint32_t part = wave * (kSlot / L);
+#pragma unroll
+    for (int c = 0; c < kPer; ++c)
+      dma16<NT>(r, lane16, __builtin_amdgcn_readfirstlane(it * kSlot + part + 1024 * c),
+                ri * kSlot + part + 1024 * c);
+  };
+  const Rsrc out = mk_rsrc(dst), none = mk_rsrc(dst, 0);
+#pragma unroll
+  for (int t = 0; t < R - 1; ++t) {
+    issue(t, t);
+    if (loader) __builtin_amdgcn_raw_buffer_store_b128(v4u{0u, 0u, 0u, 0u}, none, lane16, 0, 2);
+  }
+  uint32_t ring = 0;
+  for (uint32_t i = 0; i < n_items; ++i) {
+    if (loader) wait_vm<1 + (R - 2) * (kPer + 1)>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(i + R - 1, ring == 0 ? R - 1 : ring - 1);
+    const v4u x = *reinterpret_cast<const __attribute__((address_space(3))) v4u*>(
+        static_cast<uintptr_t>(ring * kSlot + wave * 1024 + lane16));
+    const uint32_t it = blockIdx.x + i * gridDim.x;
+    __builtin_amdgcn_raw_buffer_store_b128(x + 1u, out, lane16, it * kSlot + wave * 1024, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 0");
+    __builtin_amdgcn_sched_barrier(0);
+    ring = ring + 1 == R ? 0 : ring + 1;
+  }
+  if (loader) wait_vm<0>();
+}
+
 int g_cus = 256;
 int g_reps = 20;
 
@@ -674,6 +804,53 @@ int main(int argc, char** argv) {
       report("write 1 GiB, 16 B/lane, nt", bpc,
              time_us([&] { write_kernel<1, true><<<grid, 256>>>(out, n_copy); }), 1.0 * n_copy);
     }
+  }
+  if (want(sections, "roof")) {
+    // the guide's copy and LDS-DMA stream beside this repo's best copy
+    const uint64_t n16 = n_copy / 16;
+    report("guide: float4 copy, 1/thread, default policy", 0,
+           time_us([&] { copy_f4_kernel<1, false><<<n16 / 256, 256>>>(objs, out, n16); }), 2.0 * n_copy);
+    report("guide: float4 copy, 1/thread, nt", 0,
+           time_us([&] { copy_f4_kernel<1, true><<<n16 / 256, 256>>>(objs, out, n16); }), 2.0 * n_copy);
+    report("guide: float4 copy, 4/thread, default policy", 0,
+           time_us([&] { copy_f4_kernel<4, false><<<n16 / 1024, 256>>>(objs, out, n16); }), 2.0 * n_copy);
+    report("guide: float4 copy, 4/thread, nt", 0,
+           time_us([&] { copy_f4_kernel<4, true><<<n16 / 1024, 256>>>(objs, out, n16); }), 2.0 * n_copy);
+    report("float4 read, 1/thread, default policy", 0,
+           time_us([&] { read_f4_kernel<1, false><<<n16 / 256, 256>>>(objs, n16, sink); }), 1.0 * n_copy);
+    report("float4 read, 4/thread, nt", 0,
+           time_us([&] { read_f4_kernel<4, true><<<n16 / 1024, 256>>>(objs, n16, sink); }), 1.0 * n_copy);
+    for (int bpc : {1, 2}) {
+      const int grid = g_cus * bpc;
+      report("best copy so far: 16 B/lane grid-stride, nt", bpc,
+             time_us([&] { copy_kernel<1, true><<<grid * 2, 256>>>(objs, out, n_copy); }), 2.0 * n_copy);
+      report("guide: LDS-DMA read stream L4 D8 nt", bpc,
+             time_us([&] { dma_read_kernel<4, 8, true><<<grid, 256, 4 * 8 * 1024>>>(objs, n_copy); }), 1.0 * n_copy);
+      report("guide: LDS-DMA read stream L4 D8 default", bpc,
+             time_us([&] { dma_read_kernel<4, 8, false><<<grid, 256, 4 * 8 * 1024>>>(objs, n_copy); }), 1.0 * n_copy);
+      report("guide: LDS-DMA read stream L4 D16 nt", bpc,
+             time_us([&] { dma_read_kernel<4, 16, true><<<grid, 256, 4 * 16 * 1024>>>(objs, n_copy); }), 1.0 * n_copy);
+      report("guide: LDS-DMA read stream L4 D4 nt", bpc,
+             time_us([&] { dma_read_kernel<4, 4, true><<<grid, 256, 4 * 4 * 1024>>>(objs, n_copy); }), 1.0 * n_copy);
+    }
+    report("LDS-DMA copy W12 L4 R3 nt (product shape)", 1,
+           time_us([&] { dma_copy_kernel<12, 4, 3, true><<<g_cus, 768, 3 * 12 * 1024>>>(objs, out, n_copy); }),
+           2.0 * n_copy);
+    report("LDS-DMA copy W12 L4 R4 nt", 1,
+           time_us([&] { dma_copy_kernel<12, 4, 4, true><<<g_cus, 768, 4 * 12 * 1024>>>(objs, out, n_copy); }),
+           2.0 * n_copy);
+    report("LDS-DMA copy W8 L4 R4 nt", 1,
+           time_us([&] { dma_copy_kernel<8, 4, 4, true><<<g_cus, 512, 4 * 8 * 1024>>>(objs, out, n_copy); }),
+           2.0 * n_copy);
+    report("LDS-DMA copy W8 L4 R4 nt", 2,
+           time_us([&] { dma_copy_kernel<8, 4, 4, true><<<g_cus * 2, 512, 4 * 8 * 1024>>>(objs, out, n_copy); }),
+           2.0 * n_copy);
+    report("LDS-DMA copy W16 L4 R3 nt", 1,
+           time_us([&] { dma_copy_kernel<16, 4, 3, true><<<g_cus, 1024, 3 * 16 * 1024>>>(objs, out, n_copy); }),
+           2.0 * n_copy);
+    report("LDS-DMA copy W16 L8 R4 nt", 1,
+           time_us([&] { dma_copy_kernel<16, 8, 4, true><<<g_cus, 1024, 4 * 16 * 1024>>>(objs, out, n_copy); }),
+           2.0 * n_copy);
   }
   Shape s{objs, frags, bs_real, n_obj, bs_real / 4096, obj_stride, fs, ss};
   const double enc_bytes = double(n_obj) * s.tiles * 4096 * (K + M);
