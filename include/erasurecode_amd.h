@@ -181,7 +181,9 @@ int ecamd_call_phases(int desc, double *us, int n);
  * staging bytes held by the process, [2] single-object calls of this
  * instance that staged through HBM instead (over the pinned budget or past
  * the size limit), [3] the process's pinned budget in bytes
- * (ECAMD_PINNED_TOTAL_MB).  Returns the count written (<= n) or -errno. */
+ * (ECAMD_PINNED_TOTAL_MB), [4] single-object calls of this instance that
+ * used the caller's pages in place (ECAMD_REGISTER_CALLER).  Returns the
+ * count written (<= n) or -errno. */
 int ecamd_instance_stats(int desc, uint64_t *out, int n);
 
 /* The device-runtime error behind the calling thread's last -EBACKENDINITERR

@@ -233,11 +233,12 @@ def instance_stats(handle: "PyECLibHandle") -> dict:
     """ecamd_instance_stats: the instance's stream marks, the process's
     pinned staging bytes and budget, and its single-object calls that staged
     through HBM (tests)."""
-    out = (ctypes.c_uint64 * 4)()
-    ret = lib.ecamd_instance_stats(handle.desc, out, 4)
+    out = (ctypes.c_uint64 * 5)()
+    ret = lib.ecamd_instance_stats(handle.desc, out, 5)
     if ret < 0:
         raise_error(ret, "ecamd_instance_stats")
-    return {"marks": out[0], "pinned_bytes": out[1], "dma_calls": out[2], "pinned_budget": out[3]}
+    return {"marks": out[0], "pinned_bytes": out[1], "dma_calls": out[2], "pinned_budget": out[3],
+            "direct_calls": out[4]}
 
 
 def raise_error(ret: int, prefix: str) -> None:

@@ -87,6 +87,23 @@ struct EncodeParams {
   const void* crc_finish_tables; // CrcFinishTables for bs, device memory
   uint32_t* crc_part;
   uint32_t* crc_part_data;
+  // One object read in place (ecamd_encode_into, the caller's whole pages
+  // registered; n_obj = 1, stream kernel only): an interior 1 KiB input
+  // chunk at object offset c with [c, c + 1024) inside [direct_lo,
+  // direct_hi) is loaded from `direct` (the caller's object, device-mapped);
+  // every other input byte -- those chunks and the edge items -- from objs,
+  // the staged copy, which the caller fills for exactly those bytes.
+  // null = off.
+  const uint8_t* direct;
+  uint32_t direct_lo, direct_hi;
+  // Parity row q of this pass written in place (ecamd_encode_into, the
+  // caller's parity fragments' whole pages registered; stream kernel only):
+  // its 1 KiB interior chunk at payload offset x with [x, x + 1024) inside
+  // [dpar_lo[q], dpar_hi[q]) is stored to dpar[q] + x (the fragment's
+  // payload, device-mapped); every other parity byte to `parity` as usual.
+  // null = that row staged.
+  uint8_t* dpar[8];
+  uint32_t dpar_lo[8], dpar_hi[8];
 };
 
 // Loader / consumer kernels (ec_kernels_impl.hpp encode_dma_kernel ...):
@@ -94,8 +111,9 @@ struct EncodeParams {
 // every CU and the input offsets j * bs + x fit 32 bits.
 constexpr int kDmaMinK = 4;
 constexpr uint32_t kDmaItem = 16 * 1024;
-inline bool dma_batch(uint32_t k, uint32_t bs, uint64_t obj_len, uint32_t n_obj, int cus) {
-  if (k < static_cast<uint32_t>(kDmaMinK)) return false;
+inline bool dma_batch(uint32_t k, uint32_t bs, uint64_t obj_len, uint32_t n_obj, int cus,
+                      const void* direct = nullptr) {
+  if (k < static_cast<uint32_t>(kDmaMinK) || direct != nullptr) return false;
   if (static_cast<uint64_t>(k) * bs + 65536u > 0xFFFFFFFFull) return false;
   int64_t room = static_cast<int64_t>(obj_len) - static_cast<int64_t>(k - 1) * bs;
   if (room > static_cast<int64_t>(bs)) room = bs;
@@ -148,6 +166,14 @@ struct DecodeParams {
   const void* crc_lanes;
   const void* crc_finish_tables;
   uint32_t* crc_part;
+  // One object decoded in place (ecamd_decode_into, the caller's output
+  // pages registered; n_obj = 1, MODE kDecode, stream kernel only): a
+  // rebuilt row's 1 KiB interior chunk at object offset c with [c, c + 1024)
+  // inside [direct_lo, direct_hi) is stored to `direct` (the caller's
+  // buffer, device-mapped); every other output byte to `out` (staging, at
+  // the same offset), which the caller copies out.  null = off.
+  uint8_t* direct;
+  uint32_t direct_lo, direct_hi;
 };
 
 // Dispatch on (p.w, p.k) to the per-k instantiations (ec_dispatch.cpp).

@@ -731,6 +731,11 @@ __device__ __forceinline__ Rsrc rsrc_parity(const EncodeParams& p, uint32_t o) {
   return rsrc(p.parity + static_cast<uint64_t>(o) * p.stripe_stride,
               static_cast<int>(p.m * static_cast<uint32_t>(p.frag_stride)));
 }
+// A 1 KiB chunk at offset c is inside [lo, hi) of an in-place single
+// object (EncodeParams / DecodeParams::direct; wave-uniform).
+__device__ __forceinline__ bool in_window(const void* direct, uint32_t lo, uint32_t hi, uint32_t c) {
+  return direct != nullptr && c >= lo && c + kChunkBytes <= hi;
+}
 __device__ __forceinline__ Rsrc rsrc_data(const EncodeParams& p, uint32_t o) {
   return rsrc(p.data + static_cast<uint64_t>(o) * p.stripe_stride,
               static_cast<int>(p.k * static_cast<uint32_t>(p.frag_stride)));
@@ -886,11 +891,17 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
   uint4 buf[NB];
   const Rsrc none = rsrc(p.parity, 0);
   const uint4 zero4 = make_uint4(0, 0, 0, 0);
+  // in-place single object (EncodeParams::direct): a wave-uniform choice of
+  // descriptor per chunk, no extra instruction on the vector side
+  const Rsrc dir = rsrc(p.direct);
+  auto src = [&](Rsrc r, bool live, uint32_t soff) {
+    return live && in_window(p.direct, p.direct_lo, p.direct_hi, soff) ? dir : r;
+  };
 #pragma unroll
   for (int j = 0; j < NB; ++j) {
     if constexpr (HEAD && DATA)
       if ((SL - NB + j) % KP < K) buf_st(none, lane16, 0, zero4);
-    if (j < K) buf[j] = buf_ld<!NTL>(cur, lane16, j * p.bs + x);
+    if (j < K) buf[j] = buf_ld<!NTL>(src(cur, true, j * p.bs + x), lane16, j * p.bs + x);
   }
   if constexpr (HEAD)
 #pragma unroll
@@ -931,16 +942,25 @@ __device__ __forceinline__ void encode_interior(const EncodeParams& p) {
       }
       const int in = i + NB;  // slot refilled into this buffer
       if (in < SL) {
-        if (in % KP < K) buf[i % NB] = buf_ld<!NTL>(cur, lane16, (in % KP) * p.bs + x + kChunkBytes * (in / KP));
+        const uint32_t so = (in % KP) * p.bs + x + kChunkBytes * (in / KP);
+        if (in % KP < K) buf[i % NB] = buf_ld<!NTL>(src(cur, true, so), lane16, so);
       } else if ((in - SL) % KP < K) {
-        buf[i % NB] = buf_ld<!NTL>(nxt, lane16, ((in - SL) % KP) * p.bs + xn + kChunkBytes * ((in - SL) / KP));
+        const uint32_t so = ((in - SL) % KP) * p.bs + xn + kChunkBytes * ((in - SL) / KP);
+        buf[i % NB] = buf_ld<!NTL>(src(nxt, wn != w, so), lane16, so);
       }
       if (j == KP - 1) {  // chunk c complete: its parity rows
         F::pin(s);
         const uint32_t soff = p.row0 * p.frag_stride + kHeaderBytes + x + kChunkBytes * c;
 #pragma unroll
         for (int q = 0; q < NR; ++q)
-          if (row_live(p, q)) buf_st(par, lane16, soff + q * p.frag_stride, F::row(s, q));
+          if (row_live(p, q)) {
+            // in place (EncodeParams::dpar): a wave-uniform choice of
+            // descriptor and offset, one store either way
+            const uint32_t xc = x + kChunkBytes * c;
+            const bool dq = q < 8 && in_window(p.dpar[q & 7], p.dpar_lo[q & 7], p.dpar_hi[q & 7], xc);
+            buf_st(dq ? rsrc(p.dpar[q & 7]) : par, lane16, dq ? xc : soff + q * p.frag_stride,
+                   F::row(s, q));
+          }
         if constexpr (CRC) {
           uint32_t* part = p.crc_part + (static_cast<uint64_t>(o) * chunks + x / kChunkBytes) * p.m + p.row0;
 #pragma unroll
@@ -1607,6 +1627,8 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
     table_prefetch<F, K>(p, dn.table(), wn != w && dn.n_out() != 0 && dn.table() != st.table,
                          pre);
     const Rsrc out = rsrc_out(p.out + static_cast<uint64_t>(o) * p.out_stride, out_extent<MODE>(p));
+    // in-place single object (DecodeParams::direct): rebuilt rows' chunks
+    const Rsrc dir = rsrc_out(p.direct, out_extent<MODE>(p));
     const bool copy = MODE != kReconstruct && d.copy_inputs() != 0;
     check_desc<K, MODE>(p, d, o);
     typename F::Acc s;
@@ -1642,8 +1664,11 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
     } else {
       const uint32_t e = d.n_out();
 #pragma unroll
-      for (int q = 0; q < F::kRows; ++q)
-        drop_st(out, q < static_cast<int>(e), lane16, d.out_idx(q) * p.bs + x, F::row(s, q));
+      for (int q = 0; q < F::kRows; ++q) {
+        const uint32_t so = d.out_idx(q) * p.bs + x;
+        drop_st(in_window(p.direct, p.direct_lo, p.direct_hi, so) ? dir : out, q < static_cast<int>(e),
+                lane16, so, F::row(s, q));
+      }
     }
     if (wn == w) break;
     w = wn;
@@ -1666,10 +1691,8 @@ __device__ __forceinline__ void decode_edge_item(const DecodeParams& p, uint32_t
   const uint32_t kb = ensure_tables<F, K>(p, d, st, pre);
   const uint32_t t = tail0 + (e - o * p.edge_tiles) * kTile + threadIdx.x * 16;
   if (t >= p.bs) return;
-  // the flat stores below stay inside the object (decode: slice idx < K,
-  // window ends at object_bytes) or the payload (reconstruct)
-  ECAMD_DEVICE_ASSERT(MODE == kReconstruct || static_cast<uint64_t>(K - 1) * p.bs < p.obj_len + p.bs,
-                      "ecamd check: object %u: k * bs %u short of obj_len\n", o, p.bs);
+  // (the flat stores below stay inside the object: each is clipped to
+  // [tail0, object_bytes) of its slice, whose index check_desc has checked)
   uint8_t* out = p.out + static_cast<uint64_t>(o) * p.out_stride;
   // t < bs and 16 | t, so t + 16 <= round16(bs) <= frag_stride - 80: in bounds
   const uint8_t* in = p.frags + static_cast<uint64_t>(o) * p.stripe_stride + kHeaderBytes + t;
@@ -2337,9 +2360,24 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     // encode: round 5, k=10 m=2 256 x 4 MiB, one box: 250.7 us against 309.5
     // for the loader / consumer form (k=4 m=2: 322.3 vs 323.1;
     // profiles/r05s_km_sweep.txt)
-    if (crc || data || (NR > 2 && dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus()) &&
-                        !ab_knob("ECAMD_ENC_STREAM", 0))) {
+    // (A/B: ECAMD_ENC_DMA2=1 puts the two-row passes on the loader /
+    // consumer kernel too; ECAMD_ENC_DATA_W / _R: the full stripe's block
+    // width and ring depth)
+    if (crc || data ||
+        ((NR > 2 || ab_knob("ECAMD_ENC_DMA2", 0)) && dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus(), p.direct) &&
+         !ab_knob("ECAMD_ENC_STREAM", 0))) {
       if (static_cast<uint64_t>(K) * p.bs + 65536u > 0xFFFFFFFFull) return hipErrorInvalidValue;
+      if constexpr (kAB && K == 10 && NR == 4) {
+        const int dw = ab_knob("ECAMD_ENC_DATA_W", 12), dr = ab_knob("ECAMD_ENC_DATA_R", 3);
+        if (data && !crc && (dw != 12 || dr != 3)) {
+          if (dw == 16 && dr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, true>(p, stream, &chunks);
+          else if (dw == 12 && dr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 12, true>(p, stream, &chunks);
+          else if (dw == 8 && dr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 8, true>(p, stream, &chunks);
+          else if (dw == 8 && dr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 8, true>(p, stream, &chunks);
+          else return hipErrorInvalidValue;
+          return e;
+        }
+      }
       e = data ? launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream, &chunks)
                : launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream, &chunks);
       done = true;
@@ -2500,7 +2538,7 @@ hipError_t launch_decode_mode(DecodeParams p, hipStream_t stream) {
     if constexpr (K >= kDmaMinK && F::kRows <= kRowsPerPass) {
       const int cus = device_cus();
       if constexpr (MODE == kDecode) {
-        if (dma_batch(K, p.bs, p.obj_len, p.n_obj, cus) && !ab_knob("ECAMD_DEC_STREAM", 0))
+        if (dma_batch(K, p.bs, p.obj_len, p.n_obj, cus, p.direct) && !ab_knob("ECAMD_DEC_STREAM", 0))
           return launch_decode_dma<F, K, 3, true, 4, 12>(p, stream);
       } else if constexpr (kAB) {
         // reconstruct keeps the stream kernel: the loader / consumer form ran

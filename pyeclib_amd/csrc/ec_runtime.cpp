@@ -121,6 +121,10 @@ struct Knobs {
   // own calls (a process-wide registry: no two live registrations share a
   // page; unregistration is checked).
   bool register_caller = false;
+  // in-place calls only for objects of at least this many bytes
+  // (ECAMD_DIRECT_MIN): below it the staging copy costs less than the
+  // registration
+  size_t direct_min = size_t(256) << 10;
   long pool_slots = 0;          // ECAMD_POOL_SLOTS: decode table-set slots (0 = from 32 MiB)
   bool host_staged = false;     // ECAMD_HOST_STAGED: copy-engine host pipeline
   bool host_staged_out = false; // ECAMD_HOST_STAGED_OUT: ... with outputs staged through HBM
@@ -146,6 +150,8 @@ struct Knobs {
     k.host_chunk_mb = static_cast<int>(std::max<long>(1, env_long("ECAMD_HOST_CHUNK_MB", k.host_chunk_mb)));
     k.edge_blocks = env_on("ECAMD_EDGE_BLOCKS", true);
     k.register_caller = env_on("ECAMD_REGISTER_CALLER", false);
+    k.direct_min = static_cast<size_t>(
+        std::max<long>(0, env_long("ECAMD_DIRECT_MIN", static_cast<long>(k.direct_min))));
     k.upload_host_wait = env_on("ECAMD_UPLOAD_HOST_WAIT", true);
     return k;
   }
@@ -415,7 +421,8 @@ struct Instance {
   double phase_us[6] = {0, 0, 0, 0, 0, 0};
   DevBuf scratch;  // single-object staging
   PinBuf pin;      // single-object staging, zero-copy (small objects)
-  uint64_t dma_calls = 0;  // single-object calls that staged through HBM (ecamd_instance_stats)
+  uint64_t dma_calls = 0;     // single-object calls that staged through HBM (ecamd_instance_stats)
+  uint64_t direct_calls = 0;  // single-object calls that used the caller's pages in place
   RingSlot ring[kRing];
   int ring_pos = 0;
   UploadCache dec_cache, rec_cache, hdr_cache;
@@ -1097,6 +1104,8 @@ struct DecodeJob {
                               // copies the present data fragments itself)
   bool crc = false;           // reconstruct with inline_crc32: the launch sets each
                               // fragment's payload checksum (EncodeParams::crc_lanes)
+  uint8_t* direct = nullptr;  // one object decoded in place (DecodeParams::direct)
+  uint32_t direct_lo = 0, direct_hi = 0;
 };
 
 // Descriptors of objects [o0, o1) of a job: `passes` arrays of (o1 - o0)
@@ -1186,6 +1195,9 @@ hipError_t launch_range(Instance& I, const DecodeJob& J, int o0, int o1, uint32_
     // the kernel stores all k data slices unconditionally (DecodeMode kDecode)
     P.mode = J.dest ? 1u : (passes == 1 ? 0u : 2u);
     P.no_edge_blocks = I.knobs.edge_blocks ? 0u : 1u;
+    P.direct = J.direct;
+    P.direct_lo = J.direct_lo;
+    P.direct_hi = J.direct_hi;
     hipError_t e = launch_decode(P, stream);
     if (e != hipSuccess) return e;
   }
@@ -1369,9 +1381,19 @@ size_t crc_part_bytes(int n_obj, uint64_t bs, int rows) {
   return static_cast<size_t>(n_obj) * (bs / 1024 + 1) * rows * sizeof(uint32_t);
 }
 
+// One object's encode in place: the object read through its whole pages
+// (EncodeParams::direct) and parity rows written into theirs
+// (EncodeParams::dpar); null = staged.
+struct Direct {
+  const uint8_t* p = nullptr;
+  uint32_t lo = 0, hi = 0;
+  uint8_t* par[kMaxFragments] = {};
+  uint32_t plo[kMaxFragments] = {}, phi[kMaxFragments] = {};
+};
+
 int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t obj_len, int n_obj,
                uint8_t* parity, uint8_t* data, uint64_t frag_stride, uint64_t stripe_stride,
-               bool headers, hipStream_t stream) {
+               bool headers, hipStream_t stream, const Direct* dir = nullptr) {
   const int k = I.k, m = I.m;
   const uint64_t bs = blocksize_of(k, I.code.w, obj_len);
   if (bs == 0 && !headers) return 0;
@@ -1403,6 +1425,8 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
   // inline_crc32: every launch stores its chunks' CRC partials, and the
   // launcher runs the finishing pass (parity rows; data fragments too)
   const bool crc = headers && I.ct == CHKSUM_CRC32 && bs > 0;
+  // in place: the plain parity encode of one object only (the stream kernel)
+  if (dir && (n_obj != 1 || crc || data)) return -EINVALIDPARAMS;
   // those forms (and the full stripe) run the loader / consumer kernel for
   // k >= 4, whose input offsets j * bs + x are 32-bit (ec_kernels_impl.hpp
   // launch_encode_k)
@@ -1455,6 +1479,18 @@ int run_encode(Instance& I, const uint8_t* objs, uint64_t obj_stride, uint64_t o
     P.bs = static_cast<uint32_t>(bs);
     P.n_obj = n_obj;
     P.no_edge_blocks = I.knobs.edge_blocks ? 0u : 1u;
+    if (dir) {
+      P.direct = dir->p;
+      P.direct_lo = dir->lo;
+      P.direct_hi = dir->hi;
+      for (uint32_t q = 0; q < 8; ++q) {
+        const uint32_t r = P.row0 + q;
+        if (r >= static_cast<uint32_t>(m)) break;
+        P.dpar[q] = dir->par[r];
+        P.dpar_lo[q] = dir->plo[r];
+        P.dpar_hi[q] = dir->phi[r];
+      }
+    }
     if (bs == 0) {
       // header-only fragments: nothing for the kernel to compute
       break;
@@ -1687,33 +1723,39 @@ struct PinRegistry {
 PinRegistry* const g_pins = new PinRegistry;  // never destroyed (exit-time calls)
 constexpr uintptr_t kPage = 4096;
 
-// A caller's host buffer the kernels use in place for one call (opt-in,
-// Knobs::register_caller): registered (mapped) with hipHostRegister, and
-// unregistered by unpin() after the call's stream synchronize -- its result
-// is the call's.  pin() fails, and the caller copies through the staging
-// buffer instead, when the range cannot be registered (a page of it is held
-// by another live registration, or the range runs into unmapped memory).
+// The whole pages strictly inside a caller's host buffer, used in place by
+// the kernels for one call (opt-in, Knobs::register_caller): registered
+// (mapped) with hipHostRegister, unregistered by unpin() after the call's
+// stream synchronize -- its result is the call's.  Only pages that belong
+// to the buffer alone are registered (round 6): the partial first and last
+// pages, which other heap objects share, never are; the kernels take the
+// bytes outside [lo, hi) from the staging buffer instead (EncodeParams /
+// DecodeParams::direct).  pin() fails, and the call stages everything, when
+// the buffer holds too few whole pages, a page is held by another live
+// registration (PinRegistry), or the mapping is not the host address.
 struct CallerPin {
   void* host = nullptr;
-  uint8_t* dev = nullptr;
   uintptr_t first = 0;
+  uint32_t lo = 0, hi = 0;  // the registered bytes, as offsets into the buffer
   bool pin(const void* p, size_t n) {
-    if (n == 0) return false;
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p) & ~(kPage - 1);
-    const uintptr_t b = (reinterpret_cast<uintptr_t>(p) + n + kPage - 1) & ~(kPage - 1);
+    const uintptr_t base = reinterpret_cast<uintptr_t>(p);
+    const uintptr_t a = (base + kPage - 1) & ~(kPage - 1);
+    const uintptr_t b = (base + n) & ~(kPage - 1);
+    if (n == 0 || b <= a || b - a < 16 * kPage || n > 0xFFFFFFFFull) return false;
     PinRegistry& R = *g_pins;
     std::lock_guard<std::mutex> lk(R.mu);
     if (R.broken) return false;
     auto it = R.live.lower_bound(a);
     if (it != R.live.end() && it->first < b) return false;
     if (it != R.live.begin() && std::prev(it)->second > a) return false;
-    void* h = const_cast<void*>(p);
-    if (hipHostRegister(h, n, hipHostRegisterMapped) != hipSuccess) {
+    void* h = reinterpret_cast<void*>(a);
+    if (hipHostRegister(h, b - a, hipHostRegisterMapped) != hipSuccess) {
       (void)hipGetLastError();
       return false;
     }
     void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || d == nullptr) {
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || d != h) {
+      // the kernels address the buffer by its host address
       (void)hipGetLastError();
       if (hipHostUnregister(h) != hipSuccess) {
         (void)hipGetLastError();
@@ -1725,7 +1767,8 @@ struct CallerPin {
     R.live.emplace(a, b);
     host = h;
     first = a;
-    dev = static_cast<uint8_t*>(d);
+    lo = static_cast<uint32_t>(a - base);
+    hi = static_cast<uint32_t>(b - base);
     return true;
   }
   hipError_t unpin() {
@@ -1734,7 +1777,6 @@ struct CallerPin {
     std::lock_guard<std::mutex> lk(R.mu);
     const hipError_t e = hipHostUnregister(host);
     host = nullptr;
-    dev = nullptr;
     if (e != hipSuccess) {
       (void)hipGetLastError();
       R.broken = true;  // the range stays in `live`
@@ -1748,6 +1790,64 @@ struct CallerPin {
   CallerPin& operator=(const CallerPin&) = delete;
   ~CallerPin() { (void)unpin(); }  // error paths, after their stream synchronize
 };
+
+// Bytes of the last data slice inside an object of len bytes (the stream
+// kernels' interior tiles end at room / 4 KiB * 4 KiB of every payload).
+int64_t last_room_of(int k, uint64_t bs, uint64_t len) {
+  const int64_t room = static_cast<int64_t>(len) - static_cast<int64_t>(k - 1) * static_cast<int64_t>(bs);
+  return std::max<int64_t>(0, std::min<int64_t>(room, static_cast<int64_t>(bs)));
+}
+
+// Byte ranges [a, b) of an object, sorted and merged (the staging copies of
+// an in-place call).
+struct Ranges {
+  std::vector<std::pair<uint64_t, uint64_t>> v;
+  void add(int64_t a, int64_t b, uint64_t limit) {
+    a = std::max<int64_t>(a, 0);
+    b = std::min<int64_t>(b, static_cast<int64_t>(limit));
+    if (a < b) v.emplace_back(a, b);
+  }
+  void merge() {
+    std::sort(v.begin(), v.end());
+    size_t j = 0;
+    for (size_t i = 0; i < v.size(); ++i) {
+      if (j && v[i].first <= v[j - 1].second)
+        v[j - 1].second = std::max(v[j - 1].second, v[i].second);
+      else
+        v[j++] = v[i];
+    }
+    v.resize(j);
+  }
+};
+
+// The bytes of an object of `len` bytes (k slices of bs, the stream
+// kernels' interior tiles of 4 KiB up to `room` bytes of the last slice)
+// that an in-place launch does NOT take through the window [lo, hi): every
+// 1 KiB interior chunk of slice j not inside the window, and the edge items'
+// bytes (from tiles * 4 KiB to the slice end).  `rows`: the slices
+// concerned (null: all k).  clip: each range kept inside its own slice (the
+// copies out of a decode's staging, whose other slices hold nothing); else
+// 16 B of margin each side (the copies into an encode's staging: the edge
+// loads read aligned 16-B units).
+void outside_window(int k, uint64_t bs, uint64_t len, uint32_t lo, uint32_t hi, const bool* rows,
+                    bool clip, Ranges& R) {
+  int64_t room = static_cast<int64_t>(len) - static_cast<int64_t>(k - 1) * static_cast<int64_t>(bs);
+  room = std::max<int64_t>(0, std::min<int64_t>(room, static_cast<int64_t>(bs)));
+  const uint64_t tiles = static_cast<uint64_t>(room) / 4096;
+  const int64_t mg = clip ? 0 : 16;
+  for (int j = 0; j < k; ++j) {
+    if (rows && !rows[j]) continue;
+    const int64_t s0 = static_cast<int64_t>(j * bs);
+    const uint64_t lim = clip ? std::min<uint64_t>(s0 + bs, len) : len;
+    for (uint64_t c = 0; c < tiles * 4; ++c) {
+      const int64_t a = s0 + static_cast<int64_t>(c * 1024);
+      if (a >= lo && a + 1024 <= hi) continue;
+      R.add(a - mg, a + 1024 + mg, lim);
+    }
+    R.add(s0 + static_cast<int64_t>(tiles * 4096) - mg, s0 + static_cast<int64_t>(bs) + mg, lim);
+  }
+  R.merge();
+}
 
 // liberasurecode_encode's work for one object, into k + m caller-provided
 // fragments of bs + 80 bytes (caller holds I.mu, device set).  The kernel
@@ -1778,28 +1878,57 @@ int encode_into(Instance& I, const char* data, uint64_t len, uint8_t* const* fra
   if (bs > 0) {
     const uint64_t fs = round16(kHeaderBytes + round16(bs));
     const uint64_t obj_bytes = round16(len);
-    // the object in place when it registers (through round16(len): the edge
-    // items read whole 16-B units), the parity through the staging buffer
-    // (its stores fill whole 16-B units past bs)
+    // In place (opt-in, Knobs::register_caller): the kernel reads the
+    // caller's object through its whole interior pages (CallerPin) and takes
+    // the few bytes outside them -- the chunks at the ends, the edge items --
+    // from the staging buffer, to which only those are copied.  Otherwise
+    // the whole object is staged.  The parity goes through staging either way.
     CallerPin src;
-    const bool direct = I.knobs.register_caller && src.pin(data, obj_bytes);
-    const uint64_t staged = direct ? 0 : obj_bytes;
-    uint8_t* pin = len <= I.knobs.single_pinned_max ? I.pin.ensure(staged + fs * m) : nullptr;
+    const bool can_pin = len <= I.knobs.single_pinned_max;
+    uint8_t* pin = can_pin ? I.pin.ensure(obj_bytes + fs * m) : nullptr;
     I.dma_calls += pin == nullptr;
+    const bool want_direct = pin && I.knobs.register_caller && len >= I.knobs.direct_min;
+    const bool direct = want_direct && src.pin(data, len);
+    I.direct_calls += direct;
+    Direct dir;
+    if (direct) {
+      dir.p = reinterpret_cast<const uint8_t*>(data);
+      dir.lo = src.lo;
+      dir.hi = src.hi;
+    }
+    // the parity fragments' payloads in place too (up to 8 rows, the
+    // stream kernel's per-pass limit), each through its own whole pages
+    CallerPin parpin[8];
+    bool any_par = false;
+    for (int p = 0; want_direct && p < std::min(m, 8); ++p)
+      if (parpin[p].pin(frags[k + p] + kHeaderBytes, bs)) {
+        dir.par[p] = frags[k + p] + kHeaderBytes;
+        dir.plo[p] = parpin[p].lo;
+        dir.phi[p] = parpin[p].hi;
+        any_par = true;
+      }
     hipError_t e = hipSuccess;
-    if (!pin && (e = I.scratch.ensure(staged + fs * m)) != hipSuccess) return hip_errno(e);
+    if (!pin && (e = I.scratch.ensure(obj_bytes + fs * m)) != hipSuccess) return hip_errno(e);
     uint8_t* base = pin ? pin : I.scratch.b();
-    uint8_t* d_obj = direct ? src.dev : base;
-    uint8_t* d_par = base + staged;
-    if (!direct && pin) {
+    uint8_t* d_obj = base;
+    uint8_t* d_par = base + obj_bytes;
+    if (direct) {
+      thread_local Ranges R;
+      R.v.clear();
+      outside_window(k, bs, len, src.lo, src.hi, nullptr, false, R);
+      jobs.clear();
+      for (const auto& r : R.v) jobs.push_back({d_obj + r.first, data + r.first, r.second - r.first});
+      if (obj_bytes > len) jobs.push_back({d_obj + len, nullptr, obj_bytes - len});
+      host_copy(jobs.data(), static_cast<int>(jobs.size()));
+    } else if (pin) {
       const CopyJob in[2] = {{d_obj, data, len}, {d_obj + len, nullptr, obj_bytes - len}};
       host_copy(in, 2);
-    } else if (!direct && (e = hipMemcpyAsync(d_obj, data, len, hipMemcpyHostToDevice,
-                                              I.stream)) != hipSuccess) {
+    } else if ((e = hipMemcpyAsync(d_obj, data, len, hipMemcpyHostToDevice, I.stream)) != hipSuccess) {
       return hip_errno(e);
     }
     clk.mark(0);
-    int rc = run_encode(I, d_obj, obj_bytes, len, 1, d_par, nullptr, fs, fs * m, false, I.stream);
+    int rc = run_encode(I, d_obj, obj_bytes, len, 1, d_par, nullptr, fs, fs * m, false, I.stream,
+                        direct || any_par ? &dir : nullptr);
     if (rc < 0) {
       (void)hipStreamSynchronize(I.stream);
       return rc;
@@ -1816,11 +1945,28 @@ int encode_into(Instance& I, const char* data, uint64_t len, uint8_t* const* fra
         }
     if ((e = hipStreamSynchronize(I.stream)) != hipSuccess) return hip_errno(e);
     if ((e = src.unpin()) != hipSuccess) return hip_errno(e);
+    for (auto& pp : parpin)
+      if ((e = pp.unpin()) != hipSuccess) return hip_errno(e);
     clk.mark(3);
     if (pin) {
+      // a row written in place: only its chunks outside the window and its
+      // edge bytes came through staging
+      const uint64_t tiles = static_cast<uint64_t>(last_room_of(k, bs, len)) / 4096;
       jobs.clear();
-      for (int p = 0; p < m; ++p)
-        jobs.push_back({frags[k + p] + kHeaderBytes, d_par + p * fs + kHeaderBytes, bs});
+      for (int p = 0; p < m; ++p) {
+        uint8_t* dst = frags[k + p] + kHeaderBytes;
+        const uint8_t* from = d_par + p * fs + kHeaderBytes;
+        if (!dir.par[p]) {
+          jobs.push_back({dst, from, bs});
+          continue;
+        }
+        for (uint64_t c = 0; c < tiles * 4; ++c) {
+          const uint64_t a = c * 1024;
+          if (a >= dir.plo[p] && a + 1024 <= dir.phi[p]) continue;
+          jobs.push_back({dst + a, from + a, 1024});
+        }
+        if (tiles * 4096 < bs) jobs.push_back({dst + tiles * 4096, from + tiles * 4096, bs - tiles * 4096});
+      }
       host_copy(jobs.data(), static_cast<int>(jobs.size()));
     }
     clk.mark(4);
@@ -2022,17 +2168,22 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
   }
   const uint64_t fs = round16(kHeaderBytes + round16(bs));
   const uint64_t obj_bytes = round16(orig);
-  // the decoded object straight into the caller's buffer when it registers
-  // (the kernels' object stores are byte-exact at its end)
-  CallerPin dst;
-  const bool direct = I.knobs.register_caller && dst.pin(out, orig);
-  const size_t need = fs * (k + I.m) + (direct ? 0 : obj_bytes);
+  // In place (opt-in, Knobs::register_caller): the rebuilt slices' chunks
+  // inside the caller's whole interior pages are stored there by the kernel
+  // (CallerPin); the rest of them -- the chunks at the object's ends, the
+  // edge items -- go to the staging buffer at the same offsets and are
+  // copied out after it.  The present slices are copied by the host, from
+  // their fragments straight into the caller's buffer, beside the kernel.
+  const size_t need = fs * (k + I.m) + obj_bytes;
   uint8_t* pin = orig <= I.knobs.single_pinned_max ? I.pin.ensure(need) : nullptr;
   I.dma_calls += pin == nullptr;
+  CallerPin dst;
+  const bool direct = pin && I.knobs.register_caller && orig >= I.knobs.direct_min && dst.pin(out, orig);
+  I.direct_calls += direct;
   hipError_t e = hipSuccess;
   if (!pin && (e = I.scratch.ensure(need)) != hipSuccess) return hip_errno(e);
   uint8_t* d_frags = pin ? pin : I.scratch.b();
-  uint8_t* d_obj = direct ? dst.dev : d_frags + fs * (k + I.m);
+  uint8_t* d_obj = d_frags + fs * (k + I.m);
   uint32_t mask = 0;
   int rc = stage_fragments(I, D.P, bs, fs, d_frags, &mask, pin != nullptr);
   clk.mark(0);
@@ -2042,24 +2193,38 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
   // stored the whole object over PCIe and the host copied all of it out --
   // 4 MiB decode, 4 data fragments missing: 6 of 10 slices twice over the
   // link and through the staging copy)
-  const bool split = pin != nullptr && !direct;
+  const bool split = pin != nullptr;
   if (rc == 0) {
     DecodeJob J{d_frags, fs, fs * (k + I.m), orig, d_obj, obj_bytes, 1, &mask, nullptr, nullptr};
     J.no_copy = split;
+    if (direct) {
+      J.direct = out;
+      J.direct_lo = dst.lo;
+      J.direct_hi = dst.hi;
+    }
     rc = run_decode(I, J, I.stream);
   }
-  if (rc == 0 && orig && !pin && !direct)
+  if (rc == 0 && orig && !pin)
     if ((e = hipMemcpyAsync(out, d_obj, orig, hipMemcpyDeviceToHost, I.stream)) != hipSuccess)
       rc = hip_errno(e);
   clk.mark(1);
   thread_local std::vector<CopyJob> jobs;
+  bool rebuilt[kMaxFragments];
+  for (int j = 0; j < k; ++j) rebuilt[j] = D.P.by_idx[j] == nullptr;
   auto slices = [&](bool present) {  // data slice j of the object: present or rebuilt
     jobs.clear();
-    for (int j = 0; j < k; ++j) {
-      const uint64_t at = static_cast<uint64_t>(j) * bs;
-      if (at >= orig || (D.P.by_idx[j] != nullptr) != present) continue;
-      const uint8_t* src = present ? D.P.by_idx[j] + kHeaderBytes : d_obj + at;
-      jobs.push_back({out + at, src, std::min(bs, orig - at)});
+    if (!present && direct) {  // only what the kernel did not store in place
+      thread_local Ranges R;
+      R.v.clear();
+      outside_window(k, bs, orig, dst.lo, dst.hi, rebuilt, true, R);
+      for (const auto& r : R.v) jobs.push_back({out + r.first, d_obj + r.first, r.second - r.first});
+    } else {
+      for (int j = 0; j < k; ++j) {
+        const uint64_t at = static_cast<uint64_t>(j) * bs;
+        if (at >= orig || !rebuilt[j] != present) continue;
+        const uint8_t* src = present ? D.P.by_idx[j] + kHeaderBytes : d_obj + at;
+        jobs.push_back({out + at, src, std::min(bs, orig - at)});
+      }
     }
     host_copy(jobs.data(), static_cast<int>(jobs.size()));
   };
@@ -2246,8 +2411,9 @@ int ecamd_instance_stats(int desc, uint64_t* out, int n) {
   if (!I) return -EBACKENDNOTAVAIL;
   if (!out || n < 0) return -EINVALIDPARAMS;
   std::lock_guard<std::mutex> lk(I->mu);
-  const uint64_t v[4] = {I->marks.size(), pinned_total().load(), I->dma_calls, pinned_budget()};
-  const int c = std::min(n, 4);
+  const uint64_t v[5] = {I->marks.size(), pinned_total().load(), I->dma_calls, pinned_budget(),
+                         I->direct_calls};
+  const int c = std::min(n, 5);
   for (int i = 0; i < c; ++i) out[i] = v[i];
   return c;
 }

@@ -113,6 +113,8 @@ def test_threaded_page_sharing_calls(oracle, gpu):
             assert dec[dec_off[i]:dec_off[i] + n].tobytes() == src[src_off[i]:src_off[i] + n].tobytes()
 
     _run_threads(work, threads)
+    if os.environ.get("ECAMD_TEST_EXPECT_DIRECT") == "1":  # the in-place run (below)
+        assert sum(_native.instance_stats(h)["direct_calls"] for h in drivers) > 0
     for arr, offs, lens in ((src, src_off, sizes), (frag, frag_off, frag_sizes), (dec, dec_off, sizes)):
         mask = np.ones(arr.size, dtype=bool)
         for o, n in zip(offs, lens):
@@ -210,3 +212,22 @@ def test_pinned_staging_budget():
     r = subprocess.run([sys.executable, "-c", _BUDGET_CHILD], env=env, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0 and "budget ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_threaded_page_sharing_in_place():
+    """The same 8-thread page-sharing calls with the callers' pages used in
+    place (ECAMD_REGISTER_CALLER=1, round 6: only whole pages strictly inside
+    each caller's buffer are registered, the partial ones are staged), in a
+    child process so the knob is its own; the ~1 MiB objects take the
+    in-place path (ECAMD_DIRECT_MIN lowered so the 40-70 KB ones do too when
+    they hold 16 whole pages).  Every output against the oracle, guard bytes
+    intact, then the pageable torch copies of round 4's faulting sizes."""
+    import subprocess
+    env = dict(os.environ, ECAMD_REGISTER_CALLER="1", ECAMD_DIRECT_MIN="65536",
+               ECAMD_TEST_EXPECT_DIRECT="1")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
+                        os.path.join(ROOT, "tests", "test_gpu_caller_buffers.py") + "::test_threaded_page_sharing_calls",
+                        os.path.join(ROOT, "tests", "test_gpu_caller_buffers.py") + "::test_python_api_adjacent_bytes"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "2 passed" in r.stdout, r.stdout[-2000:]

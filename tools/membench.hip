@@ -681,6 +681,164 @@ __global__ void __launch_bounds__(W * 64) dma_copy_kernel(const uint8_t* src, ui
   if (loader) wait_vm<0>();
 }
 
+// The product's decode and encode memory patterns in the loader / consumer
+// shape (ec_kernels_impl.hpp decode_dma_kernel / encode_dma_kernel) with the
+// lookups left out.  Item = W KiB of payload positions of one object, one
+// ring slot per input.
+//   dma_dec: input j = fragment j's payload (line-aligned), stored at once to
+//            the object's slice j at j * bs (bs = 8 mod 16 at 4 MiB: half the
+//            slices misaligned); the product stores 6 present slices this way
+//            and 4 rebuilt rows at the item's end -- the same bytes.
+//   dma_enc: input j = the object's slice j (at j * bs), XORed; the 4 parity
+//            rows stored line-aligned at the item's end.
+// ORD: 0 grid-stride over the items, 1 XCD-split (encode's order).
+template <int W, int L, int R, bool NT, int ORD = 0>
+__global__ void __launch_bounds__(W * 64) dma_dec_kernel(Shape s) {
+  constexpr uint32_t kSlot = 1024u * W;
+  constexpr int kPer = W / L;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane16 = (threadIdx.x & 63) * 16;
+  const bool loader = wave < uint32_t(L);
+  const Order rg = order<ORD>(s.n_obj * s.tiles, s.tiles);
+  if (rg.begin >= rg.end) return;
+  const uint32_t n_items = (rg.end - rg.begin + rg.step - 1) / rg.step;
+  auto item_at = [&](uint32_t i, uint32_t& o, uint32_t& x0) {
+    const uint32_t w = rg.begin + (i < n_items ? i : 0) * rg.step;
+    o = __builtin_amdgcn_readfirstlane(w / s.tiles);
+    x0 = (w - o * s.tiles) * kSlot;
+  };
+  auto issue = [&](uint32_t i, int j, uint32_t ri) {
+    if (!loader) return;
+    uint32_t o, x0;
+    item_at(i, o, x0);
+    const v4u_s r = rsrc4(s.frags + uint64_t(o) * s.stripe_stride, i < n_items ? 0xFFFFFFFFu : 0u);
+    const uint32_t part = wave * (kSlot / L);
+    const uint32_t soff = __builtin_amdgcn_readfirstlane(uint32_t(j) * uint32_t(s.frag_stride) + 80 + x0 + part);
+#pragma unroll
+    for (int c = 0; c < kPer; ++c) dma16<NT>(r, lane16, soff + 1024 * c, ri * kSlot + part + 1024 * c);
+  };
+  const Rsrc none = mk_rsrc(s.objs, 0);
+#pragma unroll
+  for (int t = 0; t < R - 1; ++t) {
+    issue(t / K, t % K, t);
+    if (loader) __builtin_amdgcn_raw_buffer_store_b128(v4u{0u, 0u, 0u, 0u}, none, lane16, 0, 2);
+  }
+  uint32_t ring = 0;
+  for (uint32_t i = 0; i < n_items; ++i) {
+    uint32_t o, x0;
+    item_at(i, o, x0);
+    const Rsrc out = mk_rsrc(s.objs + uint64_t(o) * s.obj_stride);
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (loader) wait_vm<1 + (R - 2) * (kPer + 1)>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const uint32_t rn = ring == 0 ? R - 1 : ring - 1;
+      if (j + R - 1 < K)
+        issue(i, j + R - 1, rn);
+      else
+        issue(i + 1, j + R - 1 - K, rn);
+      const v4u x = *reinterpret_cast<const __attribute__((address_space(3))) v4u*>(
+          static_cast<uintptr_t>(ring * kSlot + wave * 1024 + lane16));
+      __builtin_amdgcn_raw_buffer_store_b128(x + 1u, out, lane16, uint32_t(j) * s.bs + x0 + wave * 1024, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 0");
+      __builtin_amdgcn_sched_barrier(0);
+      ring = ring + 1 == R ? 0 : ring + 1;
+    }
+  }
+  if (loader) wait_vm<0>();
+}
+
+template <int W, int L, int R, bool NT, int ORD = 1>
+__global__ void __launch_bounds__(W * 64) dma_enc_kernel(Shape s) {
+  constexpr uint32_t kSlot = 1024u * W;
+  constexpr int kPer = W / L;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t lane16 = (threadIdx.x & 63) * 16;
+  const bool loader = wave < uint32_t(L);
+  const Order rg = order<ORD>(s.n_obj * s.tiles, s.tiles);
+  if (rg.begin >= rg.end) return;
+  const uint32_t n_items = (rg.end - rg.begin + rg.step - 1) / rg.step;
+  auto item_at = [&](uint32_t i, uint32_t& o, uint32_t& x0) {
+    const uint32_t w = rg.begin + (i < n_items ? i : 0) * rg.step;
+    o = __builtin_amdgcn_readfirstlane(w / s.tiles);
+    x0 = (w - o * s.tiles) * kSlot;
+  };
+  auto issue = [&](uint32_t i, int j, uint32_t ri) {
+    if (!loader) return;
+    uint32_t o, x0;
+    item_at(i, o, x0);
+    const v4u_s r = rsrc4(s.objs + uint64_t(o) * s.obj_stride, i < n_items ? 0xFFFFFFFFu : 0u);
+    const uint32_t part = wave * (kSlot / L);
+    const uint32_t soff = __builtin_amdgcn_readfirstlane(uint32_t(j) * s.bs + x0 + part);
+#pragma unroll
+    for (int c = 0; c < kPer; ++c) dma16<NT>(r, lane16, soff + 1024 * c, ri * kSlot + part + 1024 * c);
+  };
+#pragma unroll
+  for (int t = 0; t < R - 1; ++t) issue(t / K, t % K, t);
+  uint32_t ring = 0;
+  for (uint32_t i = 0; i < n_items; ++i) {
+    uint32_t o, x0;
+    item_at(i, o, x0);
+    const Rsrc par = mk_rsrc(s.frags + uint64_t(o) * s.stripe_stride);
+    v4u acc = v4u{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      if (loader) wait_vm<kPer * (R - 2)>();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const uint32_t rn = ring == 0 ? R - 1 : ring - 1;
+      issue(i + (j + R - 1) / K, (j + R - 1) % K, rn);
+      acc ^= *reinterpret_cast<const __attribute__((address_space(3))) v4u*>(
+          static_cast<uintptr_t>(ring * kSlot + wave * 1024 + lane16));
+      ring = ring + 1 == R ? 0 : ring + 1;
+    }
+#pragma unroll
+    for (int q = 0; q < M; ++q) {
+      __builtin_amdgcn_raw_buffer_store_b128(acc + uint32_t(q), par, lane16,
+                                             uint32_t(K + q) * uint32_t(s.frag_stride) + 80 + x0 + wave * 1024, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_nop 0");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (loader) wait_vm<0>();
+}
+
+// One-shot forms of the decode / encode patterns (the float4 copy's shape):
+// one block per item (object, 4 KiB tile), no loop -- the dispatcher keeps
+// as many waves resident as fit and launches the next blocks in order, so
+// the chip sweeps memory in one compact front.  Every input of the item in
+// registers at once.
+template <bool NTL, bool NTS, bool ENC>
+__global__ void __launch_bounds__(256) oneshot_kernel(Shape s) {
+  const uint32_t w = blockIdx.x;
+  const uint32_t o = w / s.tiles, t = w - o * s.tiles;
+  const uint32_t x = t * 4096 + (threadIdx.x >> 6) * 1024 + (threadIdx.x & 63) * 16;
+  v4u v[K];
+  if constexpr (ENC) {
+    const uint8_t* src = s.objs + uint64_t(o) * s.obj_stride + x;
+#pragma unroll
+    for (int j = 0; j < K; ++j) v[j] = ld<NTL>(src + uint64_t(j) * s.bs);
+    v4u acc = v[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) acc ^= v[j];
+    uint8_t* dst = s.frags + uint64_t(o) * s.stripe_stride + K * s.frag_stride + 80 + x;
+#pragma unroll
+    for (int q = 0; q < M; ++q) st<NTS>(dst + q * s.frag_stride, acc + uint32_t(q));
+  } else {
+    const uint8_t* src = s.frags + uint64_t(o) * s.stripe_stride + 80 + x;
+#pragma unroll
+    for (int j = 0; j < K; ++j) v[j] = ld<NTL>(src + j * s.frag_stride);
+    uint8_t* dst = s.objs + uint64_t(o) * s.obj_stride + x;
+#pragma unroll
+    for (int j = 0; j < K; ++j) st<NTS>(dst + uint64_t(j) * s.bs, v[j] + 1u);
+  }
+}
+
 int g_cus = 256;
 int g_reps = 20;
 
@@ -851,6 +1009,60 @@ int main(int argc, char** argv) {
     report("LDS-DMA copy W16 L8 R4 nt", 1,
            time_us([&] { dma_copy_kernel<16, 8, 4, true><<<g_cus, 1024, 4 * 16 * 1024>>>(objs, out, n_copy); }),
            2.0 * n_copy);
+  }
+  if (want(sections, "dmapat")) {
+    // the product's decode / encode memory patterns, loader / consumer shape
+    for (uint32_t bs : {bs_real, bs_al}) {
+      auto dec = [&](auto kern, int W, const char* name) {
+        Shape d{out, frags, bs, n_obj, bs_real / (1024u * W), obj_stride, fs, ss};
+        check_shape(name, d, 1024u * W, true);
+        const double bytes = double(n_obj) * d.tiles * 1024.0 * W * (2 * K);
+        report(name, 1, time_us([&] { kern<<<g_cus, W * 64, 3 * 1024 * W + 1024 * W>>>(d); }), bytes);
+      };
+      const bool al = bs == bs_al;
+      dec(dma_dec_kernel<12, 4, 3, true>, 12, al ? "dma dec W12 R3 aligned" : "dma dec W12 R3 real (product shape)");
+      dec(dma_dec_kernel<16, 4, 3, true>, 16, al ? "dma dec W16 R3 aligned" : "dma dec W16 R3 real");
+      dec(dma_dec_kernel<12, 4, 4, true>, 12, al ? "dma dec W12 R4 aligned" : "dma dec W12 R4 real");
+      dec(dma_dec_kernel<16, 4, 3, true, 1>, 16, al ? "dma dec W16 R3 xcd aligned" : "dma dec W16 R3 xcd real");
+    }
+    auto enc = [&](auto kern, int W, const char* name) {
+      Shape e{objs, frags, bs_real, n_obj, bs_real / (1024u * W), obj_stride, fs, ss};
+      check_shape(name, e, 1024u * W);
+      const double bytes = double(n_obj) * e.tiles * 1024.0 * W * (K + M);
+      report(name, 1, time_us([&] { kern<<<g_cus, W * 64, 4 * 1024 * W>>>(e); }), bytes);
+    };
+    enc(dma_enc_kernel<12, 4, 3, true>, 12, "dma enc W12 R3 xcd (product shape)");
+    enc(dma_enc_kernel<16, 4, 3, true>, 16, "dma enc W16 R3 xcd");
+    enc(dma_enc_kernel<12, 4, 4, true>, 12, "dma enc W12 R4 xcd");
+    enc(dma_enc_kernel<16, 4, 4, true>, 16, "dma enc W16 R4 xcd");
+    enc(dma_enc_kernel<12, 4, 3, true, 0>, 12, "dma enc W12 R3 plain order");
+    enc(dma_enc_kernel<8, 4, 3, true>, 8, "dma enc W8 R3 xcd");
+  }
+  if (want(sections, "oneshot")) {
+    for (uint32_t bs : {bs_real, bs_al}) {
+      const bool al = bs == bs_al;
+      Shape d{out, frags, bs, n_obj, bs_real / 4096, obj_stride, fs, ss};
+      check_shape("oneshot dec", d, 4096, true);
+      const double db = double(n_obj) * d.tiles * 4096.0 * (2 * K);
+      const int g = n_obj * d.tiles;
+      report(al ? "oneshot dec aligned nt/nt" : "oneshot dec real nt/nt", 0,
+             time_us([&] { oneshot_kernel<true, true, false><<<g, 256>>>(d); }), db);
+      report(al ? "oneshot dec aligned def/nt" : "oneshot dec real def/nt", 0,
+             time_us([&] { oneshot_kernel<false, true, false><<<g, 256>>>(d); }), db);
+      report(al ? "oneshot dec aligned def/def" : "oneshot dec real def/def", 0,
+             time_us([&] { oneshot_kernel<false, false, false><<<g, 256>>>(d); }), db);
+      Shape e{objs, frags, bs, n_obj, bs_real / 4096, obj_stride, fs, ss};
+      check_shape("oneshot enc", e, 4096);
+      const double eb = double(n_obj) * e.tiles * 4096.0 * (K + M);
+      report(al ? "oneshot enc aligned nt/nt" : "oneshot enc real nt/nt", 0,
+             time_us([&] { oneshot_kernel<true, true, true><<<g, 256>>>(e); }), eb);
+      report(al ? "oneshot enc aligned def/nt" : "oneshot enc real def/nt", 0,
+             time_us([&] { oneshot_kernel<false, true, true><<<g, 256>>>(e); }), eb);
+    }
+    for (int bpc : {2, 4, 8, 16}) {
+      report("grid-stride copy 16 B/lane nt", bpc,
+             time_us([&] { copy_kernel<1, true><<<g_cus * bpc, 256>>>(objs, out, n_copy); }), 2.0 * n_copy);
+    }
   }
   Shape s{objs, frags, bs_real, n_obj, bs_real / 4096, obj_stride, fs, ss};
   const double enc_bytes = double(n_obj) * s.tiles * 4096 * (K + M);

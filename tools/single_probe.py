@@ -110,12 +110,22 @@ def main():
     ap.add_argument("--threads", default="")
     ap.add_argument("--pinned", default="")
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--direct", default="",
+                    help="comma list of ECAMD_REGISTER_CALLER values, one child process each "
+                         "(1: the callers' whole pages used in place)")
     a = ap.parse_args()
     sizes = [int(x) for x in a.sizes.split(",")]
+    if a.direct:
+        for d in a.direct.split(","):
+            env = dict(os.environ, ECAMD_REGISTER_CALLER=d)
+            subprocess.run([sys.executable, __file__, "--sizes", a.sizes, "--reps", str(a.reps)],
+                           env=env, check=True)
+        return
     if not a.threads and not a.pinned:
         for r in probe(sizes, a.reps):
             r["copy_threads"] = os.environ.get("ECAMD_COPY_THREADS", "default")
             r["pinned_max"] = os.environ.get("ECAMD_SINGLE_PINNED_MAX", "default")
+            r["register_caller"] = os.environ.get("ECAMD_REGISTER_CALLER", "default")
             print(json.dumps(r), flush=True)
         return
     for t in (a.threads or "4").split(","):
