@@ -108,7 +108,7 @@ def parse(argv=None):
                     help="launches of the full-stripe encode (k data + m parity fragments, "
                          "headers included: liberasurecode_encode's output) timed after the "
                          "headline steps; 0 = skip")
-    ap.add_argument("--swift-procs", default="1,4,8",
+    ap.add_argument("--swift-procs", default="1,4,15",
                     help="process counts of the Swift call-shape leg (tools/swift_calls.py: "
                          "P processes calling ECDriver.encode / decode per segment); '' = skip")
     ap.add_argument("--swift-seconds", type=float, default=1.0)
@@ -1168,7 +1168,8 @@ def main():
             "P worker processes on this GPU, each its own ECDriver(10, 4, liberasurecode_rs_vand) "
             "calling encode (or decode, 4 data fragments missing) on its own pageable segment "
             f"back to back for {args.swift_seconds} s; aggregate segment GiB/s over the span from "
-            "the first start to the last finish; us_per_call = median over processes")
+            "the first start to the last finish; us_per_call = median over processes; the "
+            "callers' buffers used in place through their whole pages (the default since round 6)")
 
     if rank == 0 and not args.no_cpu_baseline and (world == 1 or args.cpu_baseline_all):
         sample = min(args.cpu_sample or B, B)

@@ -174,6 +174,13 @@ struct DecodeParams {
   // the same offset), which the caller copies out.  null = off.
   uint8_t* direct;
   uint32_t direct_lo, direct_hi;
+  // Input c (of the first k available) of that object read in place: its
+  // 1 KiB interior chunk at payload offset x with [x, x + 1024) inside
+  // [din_lo[c], din_hi[c]) is loaded from din[c] + x (the caller's fragment
+  // payload, device-mapped); every other input byte from `frags` (staged).
+  // null = that input staged.
+  const uint8_t* din[32];
+  uint32_t din_lo[32], din_hi[32];
 };
 
 // Dispatch on (p.w, p.k) to the per-k instantiations (ec_dispatch.cpp).

@@ -1522,6 +1522,18 @@ __device__ __forceinline__ uint32_t in_pos(const DecodeParams& p, const DescU& d
   return p.compact ? static_cast<uint32_t>(c) : d.in_idx(c);
 }
 
+// Input c's 16 B per lane at payload position x (+ 16 * lane): from the
+// object's stripe, or -- an in-place single object (DecodeParams::din) --
+// from the caller's fragment when the wave's chunk is inside its window
+// (a wave-uniform choice of descriptor and offset, one load either way).
+// live: r is a real descriptor (not the zero-record one past the last item).
+__device__ __forceinline__ uint4 dec_ld(const DecodeParams& p, Rsrc r, bool live, const DescU& d, int c,
+                                        uint32_t x, uint32_t lane16) {
+  const bool dq = live && in_window(p.din[c], p.din_lo[c], p.din_hi[c], x);
+  return buf_ld(dq ? rsrc(p.din[c]) : r, lane16,
+                dq ? x : in_pos(p, d, c) * p.frag_stride + kHeaderBytes + x);
+}
+
 __device__ __forceinline__ void dec_item_pos(const DecodeParams& p, uint32_t w, uint32_t& o,
                                              uint32_t& x) {
   o = to_sgpr(w / p.tiles);
@@ -1596,8 +1608,7 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
       if (j + NB < KP) {
         if (j + NB < K) buf_st(none, lane16, 0, zero4);
       } else if (j + NB - KP < K) {
-        buf[j % NB] =
-            buf_ld(first, lane16, in_pos(p, d, j + NB - KP) * p.frag_stride + kHeaderBytes + x);
+        buf[j % NB] = dec_ld(p, first, true, d, j + NB - KP, x, lane16);
       }
     }
 #pragma unroll
@@ -1647,12 +1658,9 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
                   buf[j % NB]);
       }
       if (j + NB < KP) {
-        if (j + NB < K)
-          buf[j % NB] =
-              buf_ld(cur, lane16, in_pos(p, d, j + NB) * p.frag_stride + kHeaderBytes + x);
+        if (j + NB < K) buf[j % NB] = dec_ld(p, cur, true, d, j + NB, x, lane16);
       } else if (j + NB - KP < K) {
-        buf[j % NB] =
-            buf_ld(nxt, lane16, in_pos(p, dn, j + NB - KP) * p.frag_stride + kHeaderBytes + xn);
+        buf[j % NB] = dec_ld(p, nxt, wn != w, dn, j + NB - KP, xn, lane16);
       }
     }
     F::pin(s);

@@ -110,17 +110,20 @@ struct Knobs {
   // Round 4 (tools/single_probe.py, profiles/r04e_single_probe.txt): with the
   // parallel host copies, 4 MiB encode 279 -> 215 us through pinned staging.
   size_t single_pinned_max = size_t(64) << 20;  // ECAMD_SINGLE_PINNED_MAX
-  // Opt-in (ECAMD_REGISTER_CALLER=1): the kernels read the caller's object
-  // (encode) and write the caller's output (decode) in place, registered with
-  // hipHostRegister for the call (about 3 us for 4 MiB) instead of going
-  // through the staging buffer.  Off by default since round 5: a caller's
-  // Python buffer shares its first and last pages with other heap objects,
-  // the runtime pins whole pages, and every GPU fault of round 4 was a torch
-  // pageable copy in a process that had registered such buffers (DESIGN.md
-  // section 6b).  CallerPin keeps the opt-in path safe among this library's
-  // own calls (a process-wide registry: no two live registrations share a
-  // page; unregistration is checked).
-  bool register_caller = false;
+  // In place (default since round 6; ECAMD_REGISTER_CALLER=0 turns it
+  // off): the kernels read the caller's object (encode) and fragments
+  // (decode) and write the parity (encode) and the rebuilt slices (decode)
+  // through the whole pages strictly inside each caller buffer, registered
+  // with hipHostRegister for the call (about 2.5 us each); the partial
+  // first and last pages, which other heap objects share, never are (their
+  // bytes go through the staging buffer).  Round 4 registered whole buffers,
+  // partial pages included, and every GPU fault of that round was a torch
+  // pageable copy in a process that had done so;
+  // CallerPin keeps a process-wide registry so that no two live
+  // registrations share a page, and checks every unregistration.  Measured
+  // round 6 (tools/single_probe.py, profiles/r06f_single_probe_in_place_all.txt,
+  // one box): 4 MiB encode 185.3 -> 127.8 us, decode 181.0 -> 131.6 us.
+  bool register_caller = true;
   // in-place calls only for objects of at least this many bytes
   // (ECAMD_DIRECT_MIN): below it the staging copy costs less than the
   // registration
@@ -149,7 +152,7 @@ struct Knobs {
     k.host_streams = static_cast<int>(env_long("ECAMD_HOST_STREAMS", k.host_streams));
     k.host_chunk_mb = static_cast<int>(std::max<long>(1, env_long("ECAMD_HOST_CHUNK_MB", k.host_chunk_mb)));
     k.edge_blocks = env_on("ECAMD_EDGE_BLOCKS", true);
-    k.register_caller = env_on("ECAMD_REGISTER_CALLER", false);
+    k.register_caller = env_on("ECAMD_REGISTER_CALLER", true);
     k.direct_min = static_cast<size_t>(
         std::max<long>(0, env_long("ECAMD_DIRECT_MIN", static_cast<long>(k.direct_min))));
     k.upload_host_wait = env_on("ECAMD_UPLOAD_HOST_WAIT", true);
@@ -1106,6 +1109,14 @@ struct DecodeJob {
                               // fragment's payload checksum (EncodeParams::crc_lanes)
   uint8_t* direct = nullptr;  // one object decoded in place (DecodeParams::direct)
   uint32_t direct_lo = 0, direct_hi = 0;
+  const struct DirectIn* din = nullptr;  // its inputs read in place (DecodeParams::din)
+};
+
+// The first k available fragments of one object read in place: input c's
+// payload (device-mapped) and its window; null = staged.
+struct DirectIn {
+  const uint8_t* p[32] = {};
+  uint32_t lo[32] = {}, hi[32] = {};
 };
 
 // Descriptors of objects [o0, o1) of a job: `passes` arrays of (o1 - o0)
@@ -1198,6 +1209,12 @@ hipError_t launch_range(Instance& I, const DecodeJob& J, int o0, int o1, uint32_
     P.direct = J.direct;
     P.direct_lo = J.direct_lo;
     P.direct_hi = J.direct_hi;
+    if (J.din)
+      for (int c = 0; c < 32; ++c) {
+        P.din[c] = J.din->p[c];
+        P.din_lo[c] = J.din->lo[c];
+        P.din_hi[c] = J.din->hi[c];
+      }
     hipError_t e = launch_decode(P, stream);
     if (e != hipSuccess) return e;
   }
@@ -1724,7 +1741,7 @@ PinRegistry* const g_pins = new PinRegistry;  // never destroyed (exit-time call
 constexpr uintptr_t kPage = 4096;
 
 // The whole pages strictly inside a caller's host buffer, used in place by
-// the kernels for one call (opt-in, Knobs::register_caller): registered
+// the kernels for one call (Knobs::register_caller): registered
 // (mapped) with hipHostRegister, unregistered by unpin() after the call's
 // stream synchronize -- its result is the call's.  Only pages that belong
 // to the buffer alone are registered (round 6): the partial first and last
@@ -1878,7 +1895,7 @@ int encode_into(Instance& I, const char* data, uint64_t len, uint8_t* const* fra
   if (bs > 0) {
     const uint64_t fs = round16(kHeaderBytes + round16(bs));
     const uint64_t obj_bytes = round16(len);
-    // In place (opt-in, Knobs::register_caller): the kernel reads the
+    // In place (Knobs::register_caller): the kernel reads the
     // caller's object through its whole interior pages (CallerPin) and takes
     // the few bytes outside them -- the chunks at the ends, the edge items --
     // from the staging buffer, to which only those are copied.  Otherwise
@@ -2080,15 +2097,24 @@ int partition(const Instance& I, char** frags, int n, Partition& P) {
 
 // Upload the first k available payloads into a [k+m][fs] device image.
 // (`pinned`: d_frags is the zero-copy staging buffer, filled on the host.)
+// (`din`, pinned only: inputs read in place by the kernel -- only their
+// bytes outside the window, and the edge bytes from `tiles` 4 KiB on, are
+// staged.)
 int stage_fragments(Instance& I, const Partition& P, uint64_t bs, uint64_t fs, uint8_t* d_frags,
-                    uint32_t* mask, bool pinned) {
+                    uint32_t* mask, bool pinned, const DirectIn* din = nullptr, uint64_t tiles = 0) {
   int c = 0;
   *mask = 0;
   thread_local std::vector<CopyJob> jobs;
   jobs.clear();
   for (int i = 0; i < I.k + I.m && c < I.k; ++i) {
     if (!P.by_idx[i]) continue;
-    if (pinned) {
+    if (pinned && din && din->p[c]) {
+      uint8_t* dst = d_frags + i * fs + kHeaderBytes;
+      const uint8_t* from = P.by_idx[i] + kHeaderBytes;
+      for (uint64_t x = 0; x < tiles * 4096; x += 1024)
+        if (!(x >= din->lo[c] && x + 1024 <= din->hi[c])) jobs.push_back({dst + x, from + x, 1024});
+      if (tiles * 4096 < bs) jobs.push_back({dst + tiles * 4096, from + tiles * 4096, bs - tiles * 4096});
+    } else if (pinned) {
       jobs.push_back({d_frags + i * fs + kHeaderBytes, P.by_idx[i] + kHeaderBytes, bs});
     } else {
       hipError_t e = hipMemcpyAsync(d_frags + i * fs + kHeaderBytes, P.by_idx[i] + kHeaderBytes,
@@ -2168,7 +2194,7 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
   }
   const uint64_t fs = round16(kHeaderBytes + round16(bs));
   const uint64_t obj_bytes = round16(orig);
-  // In place (opt-in, Knobs::register_caller): the rebuilt slices' chunks
+  // In place (Knobs::register_caller): the rebuilt slices' chunks
   // inside the caller's whole interior pages are stored there by the kernel
   // (CallerPin); the rest of them -- the chunks at the object's ends, the
   // edge items -- go to the staging buffer at the same offsets and are
@@ -2178,14 +2204,32 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
   uint8_t* pin = orig <= I.knobs.single_pinned_max ? I.pin.ensure(need) : nullptr;
   I.dma_calls += pin == nullptr;
   CallerPin dst;
-  const bool direct = pin && I.knobs.register_caller && orig >= I.knobs.direct_min && dst.pin(out, orig);
+  const bool want_direct = pin && I.knobs.register_caller && orig >= I.knobs.direct_min;
+  const bool direct = want_direct && dst.pin(out, orig);
   I.direct_calls += direct;
+  // the inputs -- the first k available fragments -- in place through their
+  // own whole pages, each one that registers
+  CallerPin inpin[kMaxFragments];
+  thread_local DirectIn din;
+  din = DirectIn{};
+  bool any_in = false;
+  for (int i = 0, c = 0; want_direct && i < k + I.m && c < k; ++i) {
+    if (!D.P.by_idx[i]) continue;
+    if (inpin[c].pin(D.P.by_idx[i] + kHeaderBytes, bs)) {
+      din.p[c] = D.P.by_idx[i] + kHeaderBytes;
+      din.lo[c] = inpin[c].lo;
+      din.hi[c] = inpin[c].hi;
+      any_in = true;
+    }
+    ++c;
+  }
+  const uint64_t tiles = static_cast<uint64_t>(last_room_of(k, bs, orig)) / 4096;
   hipError_t e = hipSuccess;
   if (!pin && (e = I.scratch.ensure(need)) != hipSuccess) return hip_errno(e);
   uint8_t* d_frags = pin ? pin : I.scratch.b();
   uint8_t* d_obj = d_frags + fs * (k + I.m);
   uint32_t mask = 0;
-  int rc = stage_fragments(I, D.P, bs, fs, d_frags, &mask, pin != nullptr);
+  int rc = stage_fragments(I, D.P, bs, fs, d_frags, &mask, pin != nullptr, any_in ? &din : nullptr, tiles);
   clk.mark(0);
   // Through the pinned staging buffer, the kernel stores only the rebuilt
   // data slices: the present ones go from their fragments straight into the
@@ -2202,6 +2246,7 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
       J.direct_lo = dst.lo;
       J.direct_hi = dst.hi;
     }
+    if (any_in) J.din = &din;
     rc = run_decode(I, J, I.stream);
   }
   if (rc == 0 && orig && !pin)
@@ -2232,6 +2277,8 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
   clk.mark(2);
   if ((e = hipStreamSynchronize(I.stream)) != hipSuccess && rc == 0) rc = hip_errno(e);
   if ((e = dst.unpin()) != hipSuccess && rc == 0) rc = hip_errno(e);
+  for (auto& ip : inpin)
+    if ((e = ip.unpin()) != hipSuccess && rc == 0) rc = hip_errno(e);
   clk.mark(3);
   if (rc == 0 && orig && split) slices(false);
   clk.mark(4);

@@ -2,8 +2,9 @@
 
 Round 4's GPU faults were all torch pageable copies in
 processes that had registered callers' Python buffers with hipHostRegister;
-such buffers share their first and last pages with other heap objects.  These
-tests drive the single-object C entry points (ecamd_encode_into /
+such buffers share their first and last pages with other heap objects.  Since
+round 6 the single-object calls use the callers' buffers in place by default,
+through the whole pages strictly inside each one only.  These tests drive the single-object C entry points (ecamd_encode_into /
 ecamd_decode_into, the calls pyeclib_c.c:512-565 and :770-922 make through
 liberasurecode) on slices carved from ONE host array -- so neighbouring calls'
 inputs and outputs share pages by construction, at odd offsets -- from 8
@@ -113,8 +114,11 @@ def test_threaded_page_sharing_calls(oracle, gpu):
             assert dec[dec_off[i]:dec_off[i] + n].tobytes() == src[src_off[i]:src_off[i] + n].tobytes()
 
     _run_threads(work, threads)
-    if os.environ.get("ECAMD_TEST_EXPECT_DIRECT") == "1":  # the in-place run (below)
-        assert sum(_native.instance_stats(h)["direct_calls"] for h in drivers) > 0
+    direct = sum(_native.instance_stats(h)["direct_calls"] for h in drivers)
+    if os.environ.get("ECAMD_REGISTER_CALLER", "1") != "0":  # in place (the default): the ~1 MiB objects
+        assert direct > 0
+    else:
+        assert direct == 0
     for arr, offs, lens in ((src, src_off, sizes), (frag, frag_off, frag_sizes), (dec, dec_off, sizes)):
         mask = np.ones(arr.size, dtype=bool)
         for o, n in zip(offs, lens):
@@ -214,17 +218,19 @@ def test_pinned_staging_budget():
     assert r.returncode == 0 and "budget ok" in r.stdout, r.stdout + r.stderr
 
 
-def test_threaded_page_sharing_in_place():
-    """The same 8-thread page-sharing calls with the callers' pages used in
-    place (ECAMD_REGISTER_CALLER=1, round 6: only whole pages strictly inside
-    each caller's buffer are registered, the partial ones are staged), in a
-    child process so the knob is its own; the ~1 MiB objects take the
-    in-place path (ECAMD_DIRECT_MIN lowered so the 40-70 KB ones do too when
-    they hold 16 whole pages).  Every output against the oracle, guard bytes
-    intact, then the pageable torch copies of round 4's faulting sizes."""
+@pytest.mark.parametrize("knobs", [{"ECAMD_REGISTER_CALLER": "0"},
+                                   {"ECAMD_REGISTER_CALLER": "1", "ECAMD_DIRECT_MIN": "65536"}],
+                         ids=["staged", "in_place_from_64KiB"])
+def test_threaded_page_sharing_other_paths(knobs):
+    """The same 8-thread page-sharing calls through the other single-object
+    paths, in a child process so the knobs are its own: everything staged
+    (ECAMD_REGISTER_CALLER=0), and in place (the default since round 6: only
+    whole pages strictly inside each caller's buffer are registered, the
+    partial ones staged) from 64 KiB up, so the 40-70 KB objects take it too
+    when they hold 16 whole pages.  Every output against the oracle, guard
+    bytes intact, then the pageable torch copies of round 4's faulting sizes."""
     import subprocess
-    env = dict(os.environ, ECAMD_REGISTER_CALLER="1", ECAMD_DIRECT_MIN="65536",
-               ECAMD_TEST_EXPECT_DIRECT="1")
+    env = dict(os.environ, **knobs)
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "gpu", "-p", "no:cacheprovider",
                         os.path.join(ROOT, "tests", "test_gpu_caller_buffers.py") + "::test_threaded_page_sharing_calls",
                         os.path.join(ROOT, "tests", "test_gpu_caller_buffers.py") + "::test_python_api_adjacent_bytes"],
