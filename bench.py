@@ -1169,7 +1169,7 @@ def main():
             "calling encode (or decode, 4 data fragments missing) on its own pageable segment "
             f"back to back for {args.swift_seconds} s; aggregate segment GiB/s over the span from "
             "the first start to the last finish; us_per_call = median over processes; the "
-            "callers' buffers used in place through their whole pages (the default since round 6)")
+            "callers' buffers staged through pinned memory (ECAMD_REGISTER_CALLER=1 uses them in place)")
 
     if rank == 0 and not args.no_cpu_baseline and (world == 1 or args.cpu_baseline_all):
         sample = min(args.cpu_sample or B, B)

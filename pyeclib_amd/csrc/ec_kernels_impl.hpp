@@ -2213,7 +2213,8 @@ hipError_t encode_crc_finish(const EncodeParams& p, bool data, uint32_t chunks, 
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
           bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0, int COMB = 0,
           int CV = 0>
-hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream, uint32_t* chunks = nullptr) {
+hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream, uint32_t* chunks = nullptr,
+                             bool xcd = true) {
   set_tiles(p, last_room(p.bs, p.obj_len, K), 1024u * W * SW / kTile);
   if (chunks) *chunks = crc_chunks(p.tiles, p.tile_ch);
   const auto kern = encode_dma_kernel<F, K, NR, R, NT, L, SW, W, DATA, NOCOMP, CONTIG, RUNS, COMB, CV>;
@@ -2227,7 +2228,7 @@ hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream, uint32_t* chunk
   if (g >= 8) g &= ~7u;
   p.edge_blocks = edge_items ? e : 0;
   p.fused_edges = 1;
-  p.xcd_split = xcd_split_for(static_cast<int>(g), true);
+  p.xcd_split = xcd_split_for(static_cast<int>(g), xcd);
   hipLaunchKernelGGL(kern, dim3(g + p.edge_blocks), dim3(W * 64), lds, stream, p);
   return hipGetLastError();
 }
@@ -2279,6 +2280,8 @@ hipError_t launch_encode_ab(EncodeParams p, hipStream_t stream, bool data, uint3
       if (ring == 3 && lw == 2 && sw == 1 && nw == 16) return launch_encode_dma<F, K, NR, 3, true, 2, 1, 16>(p, stream);
       if (ring == 3 && lw == 4 && sw == 1 && nw == 12) return launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream);
       if (ring == 4 && lw == 4 && sw == 1 && nw == 12) return launch_encode_dma<F, K, NR, 4, true, 4, 1, 12>(p, stream);
+      if (ring == 4 && lw == 4 && sw == 1 && nw == 8) return launch_encode_dma<F, K, NR, 4, true, 4, 1, 8>(p, stream);
+      if (ring == 5 && lw == 4 && sw == 1 && nw == 12) return launch_encode_dma<F, K, NR, 5, true, 4, 1, 12>(p, stream);
       if (ring == -3 && lw == 4 && sw == 1 && nw == 16) return launch_encode_dma<F, K, NR, 3, false, 4, 1, 16>(p, stream);
       if (ab_knob("ECAMD_ENC_DMA_NOCOMP", 0))
         return launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, true>(p, stream);
@@ -2364,29 +2367,41 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     }
   }
   if constexpr (F::kRows <= kRowsPerPass && K >= kDmaMinK) {
-    // two-row passes (m <= 2) keep the stream kernel for the plain parity
-    // encode: round 5, k=10 m=2 256 x 4 MiB, one box: 250.7 us against 309.5
-    // for the loader / consumer form (k=4 m=2: 322.3 vs 323.1;
-    // profiles/r05s_km_sweep.txt)
-    // (A/B: ECAMD_ENC_DMA2=1 puts the two-row passes on the loader /
-    // consumer kernel too; ECAMD_ENC_DATA_W / _R: the full stripe's block
-    // width and ring depth)
+    // Two-row passes (m <= 2) too, since round 6: k=10 m=2 256 x 4 MiB, one
+    // box (profiles/r06h_ab_m2.txt), 236.5 us against 249.4 for the stream
+    // kernel, both with 0 LDS bank conflicts (r06h_sq_table_m2.txt).  Round 5
+    // had measured 309.5 against 250.7 and kept m <= 2 on the stream kernel:
+    // that was before the two-row lookups read whole 8-B entries (section
+    // 4.7 of DESIGN.md), a two-way bank conflict on every lookup.
+    // (A/B: ECAMD_ENC_STREAM2=1 keeps the two-row passes on the stream
+    // kernel, the round-5 form; ECAMD_ENC_DATA_W / _R: the full stripe's
+    // block width and ring depth)
     if (crc || data ||
-        ((NR > 2 || ab_knob("ECAMD_ENC_DMA2", 0)) && dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus(), p.direct) &&
-         !ab_knob("ECAMD_ENC_STREAM", 0))) {
+        ((NR > 2 || !ab_knob("ECAMD_ENC_STREAM2", 0)) &&
+         dma_batch(K, p.bs, p.obj_len, p.n_obj, device_cus(), p.direct) && !ab_knob("ECAMD_ENC_STREAM", 0))) {
       if (static_cast<uint64_t>(K) * p.bs + 65536u > 0xFFFFFFFFull) return hipErrorInvalidValue;
       if constexpr (kAB && K == 10 && NR == 4) {
-        const int dw = ab_knob("ECAMD_ENC_DATA_W", 12), dr = ab_knob("ECAMD_ENC_DATA_R", 3);
-        if (data && !crc && (dw != 12 || dr != 3)) {
+        const int dw = ab_knob("ECAMD_ENC_DATA_W", 8), dr = ab_knob("ECAMD_ENC_DATA_R", 4);
+        if (data && !crc && (dw != 8 || dr != 4)) {
           if (dw == 16 && dr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, true>(p, stream, &chunks);
           else if (dw == 12 && dr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 12, true>(p, stream, &chunks);
+          else if (dw == 12 && dr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream, &chunks);
           else if (dw == 8 && dr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 8, true>(p, stream, &chunks);
-          else if (dw == 8 && dr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 8, true>(p, stream, &chunks);
+          else if (dw == 8 && dr == 5) e = launch_encode_dma<F, K, NR, 5, true, 4, 1, 8, true>(p, stream, &chunks);
           else return hipErrorInvalidValue;
           return e;
         }
       }
-      e = data ? launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream, &chunks)
+      // The full stripe (data fragments stored from the ring too) at W = 8,
+      // R = 4: round 6, tools/ab_bench.py --full-stripe, one box
+      // (profiles/r06h_ab_full.txt): 455.4 us against 469.7 at W = 12, R = 3
+      // (465.4 at 12 / 4, 468.4 at 16 / 3, 528.4 at 8 / 3); the same order
+      // in membench's pattern (452.0 vs 465.6); and walking the items
+      // grid-stride without the XCD split, 448.5 against 457.3 (r06j).  The
+      // plain parity encode stays at W = 12, R = 3, XCD split: at W = 8 its
+      // two waves per SIMD cannot hide the lookups (308.0 us against 271.3
+      // at R = 4, 284.8 at R = 5; r06i_ab_alt.txt).
+      e = data ? launch_encode_dma<F, K, NR, 4, true, 4, 1, 8, true>(p, stream, &chunks, false)
                : launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream, &chunks);
       done = true;
     }
@@ -2489,6 +2504,8 @@ hipError_t launch_decode_ab(DecodeParams p, hipStream_t stream, uint32_t edge_it
     if (ab_knob("ECAMD_DEC_DMA_NOCOMP", 0) == 1) return launch_decode_dma<F, K, 3, true, 4, 12, 1>(p, stream);
     if (ab_knob("ECAMD_DEC_DMA_NOCOMP", 0) == 2) return launch_decode_dma<F, K, 3, true, 4, 12, 2>(p, stream);
     if (dring == 4 && dl == 4 && dw == 12) return launch_decode_dma<F, K, 4, true, 4, 12>(p, stream);
+    if (dring == 4 && dl == 2 && dw == 8) return launch_decode_dma<F, K, 4, true, 2, 8>(p, stream);
+    if (dring == 5 && dl == 2 && dw == 8) return launch_decode_dma<F, K, 5, true, 2, 8>(p, stream);
     if (dring == -3 && dl == 4 && dw == 16) return launch_decode_dma<F, K, 3, false>(p, stream);
     if (ab_knob("ECAMD_DEC_R3", 0))  // round 3: vector descriptor loads, old prologue
       return launch_edges_apart(decode_kernel<F, K, MODE, false, 0, false>, p, lds, items,

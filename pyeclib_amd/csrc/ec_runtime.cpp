@@ -110,20 +110,23 @@ struct Knobs {
   // Round 4 (tools/single_probe.py, profiles/r04e_single_probe.txt): with the
   // parallel host copies, 4 MiB encode 279 -> 215 us through pinned staging.
   size_t single_pinned_max = size_t(64) << 20;  // ECAMD_SINGLE_PINNED_MAX
-  // In place (default since round 6; ECAMD_REGISTER_CALLER=0 turns it
-  // off): the kernels read the caller's object (encode) and fragments
-  // (decode) and write the parity (encode) and the rebuilt slices (decode)
-  // through the whole pages strictly inside each caller buffer, registered
-  // with hipHostRegister for the call (about 2.5 us each); the partial
-  // first and last pages, which other heap objects share, never are (their
-  // bytes go through the staging buffer).  Round 4 registered whole buffers,
-  // partial pages included, and every GPU fault of that round was a torch
-  // pageable copy in a process that had done so;
-  // CallerPin keeps a process-wide registry so that no two live
-  // registrations share a page, and checks every unregistration.  Measured
-  // round 6 (tools/single_probe.py, profiles/r06f_single_probe_in_place_all.txt,
-  // one box): 4 MiB encode 185.3 -> 127.8 us, decode 181.0 -> 131.6 us.
-  bool register_caller = true;
+  // In place (opt-in, ECAMD_REGISTER_CALLER=1): the kernels read the
+  // caller's object (encode) and fragments (decode) and write the parity
+  // (encode) and the rebuilt slices (decode) through the whole pages
+  // strictly inside each caller buffer, registered with hipHostRegister for
+  // the call (about 2.5 us each); the partial first and last pages, which
+  // other heap objects share, never are (their bytes go through the staging
+  // buffer).  Measured round 6 (tools/single_probe.py,
+  // profiles/r06f_single_probe_in_place_all.txt, one box): 4 MiB encode
+  // 185.3 -> 127.8 us, decode 181.0 -> 131.6 us.  Off by default: with it
+  // on by default the GPU suite faulted once (profiles/r06k_*) exactly as in
+  // round 4 -- hipErrorIllegalAddress in a later torch pageable copy of
+  // 1.15 MB (a size the runtime pins on the fly), with no kernel of this
+  // library in flight -- so registering callers' memory, whole pages or
+  // not, is what exposes it.  CallerPin keeps a
+  // process-wide registry so that no two of this library's registrations
+  // share a page, and checks every unregistration.
+  bool register_caller = false;
   // in-place calls only for objects of at least this many bytes
   // (ECAMD_DIRECT_MIN): below it the staging copy costs less than the
   // registration
@@ -152,7 +155,7 @@ struct Knobs {
     k.host_streams = static_cast<int>(env_long("ECAMD_HOST_STREAMS", k.host_streams));
     k.host_chunk_mb = static_cast<int>(std::max<long>(1, env_long("ECAMD_HOST_CHUNK_MB", k.host_chunk_mb)));
     k.edge_blocks = env_on("ECAMD_EDGE_BLOCKS", true);
-    k.register_caller = env_on("ECAMD_REGISTER_CALLER", true);
+    k.register_caller = env_on("ECAMD_REGISTER_CALLER", false);
     k.direct_min = static_cast<size_t>(
         std::max<long>(0, env_long("ECAMD_DIRECT_MIN", static_cast<long>(k.direct_min))));
     k.upload_host_wait = env_on("ECAMD_UPLOAD_HOST_WAIT", true);
@@ -1741,7 +1744,7 @@ PinRegistry* const g_pins = new PinRegistry;  // never destroyed (exit-time call
 constexpr uintptr_t kPage = 4096;
 
 // The whole pages strictly inside a caller's host buffer, used in place by
-// the kernels for one call (Knobs::register_caller): registered
+// the kernels for one call (opt-in, Knobs::register_caller): registered
 // (mapped) with hipHostRegister, unregistered by unpin() after the call's
 // stream synchronize -- its result is the call's.  Only pages that belong
 // to the buffer alone are registered (round 6): the partial first and last
@@ -1895,7 +1898,7 @@ int encode_into(Instance& I, const char* data, uint64_t len, uint8_t* const* fra
   if (bs > 0) {
     const uint64_t fs = round16(kHeaderBytes + round16(bs));
     const uint64_t obj_bytes = round16(len);
-    // In place (Knobs::register_caller): the kernel reads the
+    // In place (opt-in, Knobs::register_caller): the kernel reads the
     // caller's object through its whole interior pages (CallerPin) and takes
     // the few bytes outside them -- the chunks at the ends, the edge items --
     // from the staging buffer, to which only those are copied.  Otherwise
@@ -2194,7 +2197,7 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
   }
   const uint64_t fs = round16(kHeaderBytes + round16(bs));
   const uint64_t obj_bytes = round16(orig);
-  // In place (Knobs::register_caller): the rebuilt slices' chunks
+  // In place (opt-in, Knobs::register_caller): the rebuilt slices' chunks
   // inside the caller's whole interior pages are stored there by the kernel
   // (CallerPin); the rest of them -- the chunks at the object's ends, the
   // edge items -- go to the staging buffer at the same offsets and are

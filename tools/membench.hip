@@ -751,7 +751,9 @@ __global__ void __launch_bounds__(W * 64) dma_dec_kernel(Shape s) {
   if (loader) wait_vm<0>();
 }
 
-template <int W, int L, int R, bool NT, int ORD = 1>
+// DATA: the full stripe -- every input chunk also stored to its data
+// fragment's (line-aligned) payload as it is read from the ring.
+template <int W, int L, int R, bool NT, int ORD = 1, bool DATA = false>
 __global__ void __launch_bounds__(W * 64) dma_enc_kernel(Shape s) {
   constexpr uint32_t kSlot = 1024u * W;
   constexpr int kPer = W / L;
@@ -792,8 +794,16 @@ __global__ void __launch_bounds__(W * 64) dma_enc_kernel(Shape s) {
       asm volatile("" ::: "memory");
       const uint32_t rn = ring == 0 ? R - 1 : ring - 1;
       issue(i + (j + R - 1) / K, (j + R - 1) % K, rn);
-      acc ^= *reinterpret_cast<const __attribute__((address_space(3))) v4u*>(
+      const v4u xin = *reinterpret_cast<const __attribute__((address_space(3))) v4u*>(
           static_cast<uintptr_t>(ring * kSlot + wave * 1024 + lane16));
+      acc ^= xin;
+      if constexpr (DATA) {
+        __builtin_amdgcn_raw_buffer_store_b128(xin, par, lane16,
+                                               uint32_t(j) * uint32_t(s.frag_stride) + 80 + x0 + wave * 1024, 2);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 0");
+        __builtin_amdgcn_sched_barrier(0);
+      }
       ring = ring + 1 == R ? 0 : ring + 1;
     }
 #pragma unroll
@@ -1017,19 +1027,21 @@ int main(int argc, char** argv) {
         Shape d{out, frags, bs, n_obj, bs_real / (1024u * W), obj_stride, fs, ss};
         check_shape(name, d, 1024u * W, true);
         const double bytes = double(n_obj) * d.tiles * 1024.0 * W * (2 * K);
-        report(name, 1, time_us([&] { kern<<<g_cus, W * 64, 3 * 1024 * W + 1024 * W>>>(d); }), bytes);
+        report(name, 1, time_us([&] { kern<<<g_cus, W * 64, 5 * 1024 * W>>>(d); }), bytes);
       };
       const bool al = bs == bs_al;
       dec(dma_dec_kernel<12, 4, 3, true>, 12, al ? "dma dec W12 R3 aligned" : "dma dec W12 R3 real (product shape)");
       dec(dma_dec_kernel<16, 4, 3, true>, 16, al ? "dma dec W16 R3 aligned" : "dma dec W16 R3 real");
       dec(dma_dec_kernel<12, 4, 4, true>, 12, al ? "dma dec W12 R4 aligned" : "dma dec W12 R4 real");
       dec(dma_dec_kernel<16, 4, 3, true, 1>, 16, al ? "dma dec W16 R3 xcd aligned" : "dma dec W16 R3 xcd real");
+      dec(dma_dec_kernel<8, 4, 4, true>, 8, al ? "dma dec W8 R4 aligned" : "dma dec W8 R4 real");
+      dec(dma_dec_kernel<8, 4, 5, true>, 8, al ? "dma dec W8 R5 aligned" : "dma dec W8 R5 real");
     }
     auto enc = [&](auto kern, int W, const char* name) {
       Shape e{objs, frags, bs_real, n_obj, bs_real / (1024u * W), obj_stride, fs, ss};
       check_shape(name, e, 1024u * W);
       const double bytes = double(n_obj) * e.tiles * 1024.0 * W * (K + M);
-      report(name, 1, time_us([&] { kern<<<g_cus, W * 64, 4 * 1024 * W>>>(e); }), bytes);
+      report(name, 1, time_us([&] { kern<<<g_cus, W * 64, 5 * 1024 * W>>>(e); }), bytes);
     };
     enc(dma_enc_kernel<12, 4, 3, true>, 12, "dma enc W12 R3 xcd (product shape)");
     enc(dma_enc_kernel<16, 4, 3, true>, 16, "dma enc W16 R3 xcd");
@@ -1037,6 +1049,30 @@ int main(int argc, char** argv) {
     enc(dma_enc_kernel<16, 4, 4, true>, 16, "dma enc W16 R4 xcd");
     enc(dma_enc_kernel<12, 4, 3, true, 0>, 12, "dma enc W12 R3 plain order");
     enc(dma_enc_kernel<8, 4, 3, true>, 8, "dma enc W8 R3 xcd");
+    // slice misalignment (bs = 8 mod 16 at 4 MiB, k = 10: half the slices)
+    for (uint32_t b : {bs_real + 2, bs_al}) {
+      Shape e{objs, frags, b, n_obj, bs_real / 12288u, obj_stride, fs, ss};
+      check_shape("enc mis", e, 12288u);
+      const double bytes = double(n_obj) * e.tiles * 12288.0 * (K + M);
+      report(b == bs_al ? "dma enc W12 R3 xcd, slices 128-B aligned" : "dma enc W12 R3 xcd, bs = 10 mod 16",
+             1, time_us([&] { dma_enc_kernel<12, 4, 3, true><<<g_cus, 768, 5 * 12288>>>(e); }), bytes);
+    }
+    enc(dma_enc_kernel<8, 4, 4, true>, 8, "dma enc W8 R4 xcd");
+    enc(dma_enc_kernel<8, 4, 5, true>, 8, "dma enc W8 R5 xcd");
+    // the full stripe (k data + m parity fragments): bytes = L + (k + m) x payload
+    auto full = [&](auto kern, int W, int R, const char* name) {
+      Shape e{objs, frags, bs_real, n_obj, bs_real / (1024u * W), obj_stride, fs, ss};
+      check_shape(name, e, 1024u * W);
+      const double bytes = double(n_obj) * e.tiles * 1024.0 * W * (2 * K + M);
+      report(name, 1, time_us([&] { kern<<<g_cus, W * 64, R * 1024 * W>>>(e); }), bytes);
+    };
+    full(dma_enc_kernel<12, 4, 3, true, 1, true>, 12, 3, "dma full stripe W12 R3 xcd (product shape)");
+    full(dma_enc_kernel<16, 4, 3, true, 1, true>, 16, 3, "dma full stripe W16 R3 xcd");
+    full(dma_enc_kernel<12, 4, 4, true, 1, true>, 12, 4, "dma full stripe W12 R4 xcd");
+    full(dma_enc_kernel<8, 4, 4, true, 1, true>, 8, 4, "dma full stripe W8 R4 xcd");
+    full(dma_enc_kernel<12, 4, 3, true, 0, true>, 12, 3, "dma full stripe W12 R3 plain order");
+    full(dma_enc_kernel<8, 4, 5, true, 1, true>, 8, 5, "dma full stripe W8 R5 xcd");
+    full(dma_enc_kernel<8, 4, 4, true, 0, true>, 8, 4, "dma full stripe W8 R4 plain order");
   }
   if (want(sections, "oneshot")) {
     for (uint32_t bs : {bs_real, bs_al}) {
