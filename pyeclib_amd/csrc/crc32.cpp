@@ -130,6 +130,7 @@ void build_crc_lane_tables(bool legacy, CrcLaneTables* out) {
     const Mat tail = zeros(15 - i, legacy);
     for (int h = 0; h < 2; ++h)
       for (uint32_t v = 0; v < 16; ++v) out->raw16[2 * i + h][v] = apply(tail, tb.t[0][(v << (4 * h)) & 0xFF]);
+    for (uint32_t v = 0; v < 256; ++v) out->rawb[i][v] = apply(tail, tb.t[0][v]);
   }
   for (int l = 0; l < 64; ++l) {
     uint32_t t[8][16];

@@ -37,6 +37,8 @@ struct CrcLaneTables {
   uint32_t raw16[32][16];     // raw CRC of a 16-byte piece, per nibble position
   uint32_t lane[8][16][64];   // Z_{16 (63 - l)}: [q][v][lane], lane-minor, so the
                               // 64 lanes of a lookup hit 64 different banks
+  uint32_t rawb[16][256];     // raw CRC of a 16-byte piece, per byte position:
+                              // one lookup per byte instead of two (round 6)
 };
 static_assert(sizeof(CrcLaneTables) % 16 == 0, "copied to LDS in 16-B pieces");
 

@@ -93,6 +93,38 @@ __device__ __forceinline__ uint32_t raw_dword(uint32_t w, int d, uint32_t tab) {
   return a;
 }
 
+// Byte b of x, times 4 (a byte-indexed table's offset): one SDWA shift.
+template <int B>
+__device__ __forceinline__ uint32_t byte4(uint32_t x) {
+  uint32_t r;
+  if constexpr (B == 0)
+    asm("v_lshlrev_b32_sdwa %0, %2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+        : "=v"(r) : "v"(x), "v"(2u));
+  else if constexpr (B == 1)
+    asm("v_lshlrev_b32_sdwa %0, %2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+        : "=v"(r) : "v"(x), "v"(2u));
+  else if constexpr (B == 2)
+    asm("v_lshlrev_b32_sdwa %0, %2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+        : "=v"(r) : "v"(x), "v"(2u));
+  else
+    asm("v_lshlrev_b32_sdwa %0, %2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+        : "=v"(r) : "v"(x), "v"(2u));
+  return r;
+}
+
+// raw_dword by byte-indexed tables (CrcLaneTables::rawb; `tab` = the lane
+// tables' LDS base): 4 lookups instead of 8, one SDWA shift each for the
+// address.  A 256-entry table read by 64 lanes at random shares banks
+// (4 entries per bank), which nibble tables never do.
+__device__ __forceinline__ uint32_t raw_dword_b(uint32_t w, int d, uint32_t tab) {
+  const uint32_t t = tab + static_cast<uint32_t>(offsetof(CrcLaneTables, rawb)) + 4096u * d;
+  const uint32_t a = lds32(t + byte4<0>(w)) ^ lds32(t + 1024 + byte4<1>(w)) ^
+                     lds32(t + 2048 + byte4<2>(w)) ^ lds32(t + 3072 + byte4<3>(w));
+  uint32_t r = a;
+  asm volatile("" : "+v"(r));
+  return r;
+}
+
 // Z_{16 (63 - l)}(r) for this lane: the lane-minor tables at LDS byte
 // `tab`, lane4 = 4 * lane.
 __device__ __forceinline__ uint32_t lane_map(uint32_t r, uint32_t tab, uint32_t lane4) {

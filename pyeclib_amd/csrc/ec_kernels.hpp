@@ -182,6 +182,7 @@ struct DecodeParams {
   const uint8_t* din[32];
   uint32_t din_lo[32], din_hi[32];
 };
+constexpr int kDinMax = 16;  // inputs read in place only for k <= 16
 
 // Dispatch on (p.w, p.k) to the per-k instantiations (ec_dispatch.cpp).
 hipError_t launch_encode(const EncodeParams& p, hipStream_t stream);

@@ -1230,7 +1230,9 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
     const int q = u / 5, d = u % 5;
     if (d < 4) {
       const uint32_t w = d == 0 ? crow[q].x : d == 1 ? crow[q].y : d == 2 ? crow[q].z : crow[q].w;
-      cacc[q] ^= crcdev::raw_dword(w, d, dma_ring_base<F, K>());
+      // CV 3 (A/B): byte-indexed tables, 4 lookups per dword instead of 8
+      cacc[q] ^= CV == 3 ? crcdev::raw_dword_b(w, d, dma_ring_base<F, K>())
+                         : crcdev::raw_dword(w, d, dma_ring_base<F, K>());
     } else if (static_cast<uint32_t>(q) < p.nrows) {
       crc_store(cpart + q, crcdev::wave_xor(crcdev::lane_map(
                                cacc[q], dma_ring_base<F, K>() + offsetof(CrcLaneTables, lane), lane4)));
@@ -1269,7 +1271,7 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
                       crcdev::chunk_crc(x, dma_ring_base<F, K>(), lane4));
         }
       }
-      if constexpr (SW == 1 && CV == 0) {
+      if constexpr (SW == 1 && (CV == 0 || CV == 3)) {
         if (cpend) {  // the previous item's CRC steps [kCrcSteps j / K, kCrcSteps (j + 1) / K)
 #pragma unroll
           for (int u = j * kCrcSteps / K; u < (j + 1) * kCrcSteps / K; ++u) crc_step(u);
@@ -1286,7 +1288,7 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
         buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, F::row(s[c], q));
       if (crc) {
         uint32_t* part = p.crc_part + (static_cast<uint64_t>(o) * chunks + x0 / 1024 + wave * SW + c) * p.m + p.row0;
-        if constexpr (SW == 1 && CV == 0) {  // taken during the next item (or after the last)
+        if constexpr (SW == 1 && (CV == 0 || CV == 3)) {  // taken during the next item (or after the last)
 #pragma unroll
           for (int q = 0; q < NR; ++q) {
             crow[q] = F::row(s[c], q);
@@ -1304,7 +1306,7 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
       F::zero(s[c]);
     }
   }
-  if constexpr (SW == 1 && CV == 0) {
+  if constexpr (SW == 1 && (CV == 0 || CV == 3)) {
     if (cpend) {  // the block's last item
 #pragma unroll
       for (int u = 0; u < kCrcSteps; ++u) crc_step(u);
@@ -1527,9 +1529,12 @@ __device__ __forceinline__ uint32_t in_pos(const DecodeParams& p, const DescU& d
 // from the caller's fragment when the wave's chunk is inside its window
 // (a wave-uniform choice of descriptor and offset, one load either way).
 // live: r is a real descriptor (not the zero-record one past the last item).
+// Only for k <= kDinMax: with more inputs the per-input pointers pushed the
+// prime-k kernels past the SGPRs (k = 17 spilled 68 B per lane).
+template <int K>
 __device__ __forceinline__ uint4 dec_ld(const DecodeParams& p, Rsrc r, bool live, const DescU& d, int c,
                                         uint32_t x, uint32_t lane16) {
-  const bool dq = live && in_window(p.din[c], p.din_lo[c], p.din_hi[c], x);
+  const bool dq = K <= kDinMax && live && in_window(p.din[c & 31], p.din_lo[c & 31], p.din_hi[c & 31], x);
   return buf_ld(dq ? rsrc(p.din[c]) : r, lane16,
                 dq ? x : in_pos(p, d, c) * p.frag_stride + kHeaderBytes + x);
 }
@@ -1608,7 +1613,7 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
       if (j + NB < KP) {
         if (j + NB < K) buf_st(none, lane16, 0, zero4);
       } else if (j + NB - KP < K) {
-        buf[j % NB] = dec_ld(p, first, true, d, j + NB - KP, x, lane16);
+        buf[j % NB] = dec_ld<K>(p, first, true, d, j + NB - KP, x, lane16);
       }
     }
 #pragma unroll
@@ -1658,9 +1663,9 @@ __device__ __forceinline__ void decode_interior(const DecodeParams& p, Slots& st
                   buf[j % NB]);
       }
       if (j + NB < KP) {
-        if (j + NB < K) buf[j % NB] = dec_ld(p, cur, true, d, j + NB, x, lane16);
+        if (j + NB < K) buf[j % NB] = dec_ld<K>(p, cur, true, d, j + NB, x, lane16);
       } else if (j + NB - KP < K) {
-        buf[j % NB] = dec_ld(p, nxt, wn != w, dn, j + NB - KP, xn, lane16);
+        buf[j % NB] = dec_ld<K>(p, nxt, wn != w, dn, j + NB - KP, xn, lane16);
       }
     }
     F::pin(s);
@@ -2361,6 +2366,7 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
       else if (cv == 2 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 2>(p, stream, &chunks);
       else if (cv == 0 && cr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 12>(p, stream, &chunks);
       else if (cv == 1 && cr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 12, false, false, false, 0, 0, 1>(p, stream, &chunks);
+      else if (cv == 3 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 3>(p, stream, &chunks);
       else return hipErrorInvalidValue;
       if (e != hipSuccess) return e;
       return encode_crc_finish<K>(p, data, chunks, stream);

@@ -664,7 +664,11 @@ struct Instance {
     if ((e = hipMemcpyAsync(r->dev.p, r->host, n, hipMemcpyHostToDevice, ustream)) != hipSuccess)
       return e;
     if ((e = hipEventRecord(r->cev, ustream)) != hipSuccess) return e;
-    if (knobs.upload_host_wait) return hipEventSynchronize(r->cev);
+    // After a pool recycle the upload stream may hold a GPU-side wait behind
+    // queued kernels (pool_commit); a host wait would then block on them, so
+    // the launch waits on the GPU instead (round-5 advice).
+    const bool behind_gpu = pool_gen_pending && hipEventQuery(pool_gen_ev) != hipSuccess;
+    if (knobs.upload_host_wait && !behind_gpu) return hipEventSynchronize(r->cev);
     return hipStreamWaitEvent(s, r->cev, 0);
   }
   hipError_t ring_release(RingSlot* r, hipStream_t s) {
@@ -2216,7 +2220,7 @@ int decode_into(Instance& I, const DecodeIn& D, uint8_t* out) {
   thread_local DirectIn din;
   din = DirectIn{};
   bool any_in = false;
-  for (int i = 0, c = 0; want_direct && i < k + I.m && c < k; ++i) {
+  for (int i = 0, c = 0; want_direct && k <= kDinMax && i < k + I.m && c < k; ++i) {
     if (!D.P.by_idx[i]) continue;
     if (inpin[c].pin(D.P.by_idx[i] + kHeaderBytes, bs)) {
       din.p[c] = D.P.by_idx[i] + kHeaderBytes;
