@@ -130,8 +130,36 @@ void build_crc_lane_tables(bool legacy, CrcLaneTables* out) {
     const Mat tail = zeros(15 - i, legacy);
     for (int h = 0; h < 2; ++h)
       for (uint32_t v = 0; v < 16; ++v) out->raw16[2 * i + h][v] = apply(tail, tb.t[0][(v << (4 * h)) & 0xFF]);
-    for (uint32_t v = 0; v < 256; ++v) out->rawb[i][v] = apply(tail, tb.t[0][v]);
   }
+  // Matrix-core form.  A operand of v_mfma_i32_32x32x32_i8, plane b: lane L
+  // holds its piece's 16 bytes masked to bit b (value 2^b or 0), row L mod 32,
+  // K block L / 32 -- so row r sums lanes r and r + 32, the latter 512 bytes
+  // nearer the chunk's end.  B, plane b: lane L = n + 32 g, byte e = bit n of
+  // Z_{512 (1 - g)}(raw16 of bit b of byte e), times 2^(7 - b): every product
+  // is then 128 (mod 256) times a 0/1 term, and bit 7 of the i32 sum is its
+  // parity (+-128 alike: -128 = 128 mod 256).
+  const Mat shift[2] = {zeros(512, legacy), identity()};
+  Mat tails[16], rows[32];
+  for (int e = 0; e < 16; ++e) tails[e] = zeros(15 - e, legacy);
+  for (int r = 0; r < 32; ++r) rows[r] = zeros(uint64_t(16) * (31 - r), legacy);
+  for (int b = 0; b < 8; ++b)
+    for (int L = 0; L < 64; ++L)
+      for (int e = 0; e < 16; ++e) {
+        const uint32_t v = apply(shift[L / 32], apply(tails[e], tb.t[0][1u << b]));
+        out->mfb[b][L][e] = (v >> (L % 32) & 1) ? static_cast<int8_t>(static_cast<uint8_t>(0x80u >> b)) : 0;
+      }
+  // Second stage.  Accumulator j of lane l holds C[8 (j / 4) + 4 (l / 32) +
+  // j mod 4][l mod 32]: row r's sum for output bit n = l mod 32, i.e. bit n of
+  // u_r, and raw(chunk) = XOR_r Z_{16 (31 - r)}(u_r).  Nibble q of lane l =
+  // the parities of its accumulators 4q .. 4q + 3.
+  for (int l = 0; l < 64; ++l)
+    for (int q = 0; q < 4; ++q)
+      for (uint32_t v = 0; v < 16; ++v) {
+        uint32_t a = 0;
+        for (int i = 0; i < 4; ++i)
+          if (v >> i & 1) a ^= rows[8 * q + 4 * (l / 32) + i].col[l % 32];
+        out->mst[q][v][l] = a;
+      }
   for (int l = 0; l < 64; ++l) {
     uint32_t t[8][16];
     nibble_tables(zeros(uint64_t(16) * (63 - l), legacy), t);

@@ -37,10 +37,18 @@ struct CrcLaneTables {
   uint32_t raw16[32][16];     // raw CRC of a 16-byte piece, per nibble position
   uint32_t lane[8][16][64];   // Z_{16 (63 - l)}: [q][v][lane], lane-minor, so the
                               // 64 lanes of a lookup hit 64 different banks
-  uint32_t rawb[16][256];     // raw CRC of a 16-byte piece, per byte position:
-                              // one lookup per byte instead of two (round 6)
+  // The matrix-core form (round 6, crc_device.hpp mfma_*): the chunk's 8192
+  // bits times a 0/1 matrix on v_mfma_i32_32x32x32_i8, one bit plane of the
+  // 16 bytes per instruction, the parity of each sum in bit 7 of its i32.
+  uint32_t mst[4][16][64];    // second stage: lane l's 16 row sums -> Z_{16 (31 - r)}
+                              // of its column's bit, by nibble [q][v][lane]
+  int8_t mfb[8][64][16];      // B operands: [bit plane][lane][byte]; read into
+                              // registers from device memory, never copied to LDS
 };
 static_assert(sizeof(CrcLaneTables) % 16 == 0, "copied to LDS in 16-B pieces");
+// What the kernels copy to LDS: everything before mfb.
+constexpr unsigned kCrcLdsBytes = static_cast<unsigned>(offsetof(CrcLaneTables, mfb));
+static_assert(kCrcLdsBytes % 16 == 0, "copied to LDS in 16-B pieces");
 
 // The finishing pass (ec_crc.hip) shifts every chunk's raw CRC to the end
 // of the bs-byte payload -- chunk c ends at 1024 (c + 1), so by Z_r after

@@ -828,7 +828,7 @@ __device__ __forceinline__ void encode_edge_item(const EncodeParams& p, uint32_t
 // threads at every run end behind block barriers: 1.21-1.26x the plain
 // encode, 10 % of it the order; profiles/r04n_ab_contig.txt.)  The lane
 // tables (CrcLaneTables, 34 KiB) sit in LDS after the GF tables.
-constexpr uint32_t kCrcLaneBytes = sizeof(CrcLaneTables);
+constexpr uint32_t kCrcLaneBytes = kCrcLdsBytes;
 template <class F, int K>
 __host__ __device__ constexpr uint32_t crc_lds_base() {
   return (K * F::kTableBytes + 255u) & ~255u;
@@ -1127,10 +1127,12 @@ __host__ __device__ constexpr uint32_t dma_lds_bytes(bool crc = false) {
 // COMB-item stride could use); G / COMB objects in flight.
 // CV (A/B, inline CRC): 0 = the parity chunks' CRC steps deferred over the
 // next item's slots (the product), 1 = taken at the item's end, 2 = at the
-// item's end with unfenced raw16 lookups (crcdev::raw16_free).
+// item's end with unfenced raw16 lookups (crcdev::raw16_free), 4 = deferred
+// like 0, on the matrix cores (crcdev::mfma_*: 8 v_mfma_i32_32x32x32_i8 and 4
+// lookups per row chunk instead of 40 lookups).
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
           bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0, int COMB = 0,
-          int CV = 0>
+          int CV = 6>
 __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   static_assert(R >= 2 && R <= K + 1, "ring of 2 .. K + 1 slots");
   static_assert(L == 2 || L == 4 || L == 8 || L == 16, "loader waves");
@@ -1221,18 +1223,53 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   // no wave carries a burst of lookups into a ring barrier -- taken all at
   // the item's end they held the ring for ~3.8 K LDS cycles per CU and item
   // (the CRC encode ran 1.28x the plain one; profiles/r05b_*).
-  constexpr int kCrcSteps = 5 * NR;
+  // CV 4: 9 steps per row -- its 8 bit planes on the matrix cores into one
+  // accumulator (rows one after another), then the 4 lookups and the store.
+  // CV 6 (the product): as 4, each row's lookups kept per lane and one wave
+  // XOR for all the rows at the end (crcdev::wave_xor4; a last step).
+  constexpr bool kMf = CV == 4 || CV == 6;
+  constexpr bool kMf4 = CV == 6;
+  constexpr int kPerRow = kMf ? 9 : 5;
+  constexpr int kCrcSteps = kPerRow * NR + (kMf4 ? 1 : 0);
+  static_assert(!kMf4 || NR <= 4, "one joint wave XOR");
+  uint32_t cfin[kMf4 ? 4 : 1] = {};
+  uint32_t dfin[kMf4 && DATA ? 4 : 1] = {};
   uint4 crow[NR];
   uint32_t cacc[NR];
   uint32_t* cpart = p.crc_part;
   bool cpend = false;
+  crcdev::mfma_v4i mb[kMf ? 8 : 1];
+  crcdev::mfma_v16i macc = {};
+  if constexpr (kMf) {
+    if (crc) crcdev::mfma_load_b(p.crc_lanes, lane_id(), mb);
+  }
   auto crc_step = [&](int u) {
-    const int q = u / 5, d = u % 5;
+    if constexpr (kMf4) {
+      if (u == kPerRow * NR) {
+        const uint32_t t = crcdev::wave_xor4(cfin[0], cfin[1], cfin[2], cfin[3], lane_id());
+        if (lane_id() < p.nrows && lane_id() < static_cast<uint32_t>(NR)) cpart[lane_id()] = t;
+        return;
+      }
+      const int q = u / kPerRow, d = u % kPerRow;
+      if (d < 8)
+        macc = crcdev::mfma_plane(crow[q], d, mb[d], d == 0 ? crcdev::mfma_v16i{} : macc);
+      else
+        cfin[q] = crcdev::mfma_lanes(macc, dma_ring_base<F, K>() + offsetof(CrcLaneTables, mst), lane4);
+      return;
+    }
+    if constexpr (kMf) {
+      const int q = u / kPerRow, d = u % kPerRow;
+      if (d < 8) {
+        macc = crcdev::mfma_plane(crow[q], d, mb[d], d == 0 ? crcdev::mfma_v16i{} : macc);
+      } else if (static_cast<uint32_t>(q) < p.nrows) {
+        crc_store(cpart + q, crcdev::mfma_finish(macc, dma_ring_base<F, K>() + offsetof(CrcLaneTables, mst), lane4));
+      }
+      return;
+    }
+    const int q = u / kPerRow, d = u % kPerRow;
     if (d < 4) {
       const uint32_t w = d == 0 ? crow[q].x : d == 1 ? crow[q].y : d == 2 ? crow[q].z : crow[q].w;
-      // CV 3 (A/B): byte-indexed tables, 4 lookups per dword instead of 8
-      cacc[q] ^= CV == 3 ? crcdev::raw_dword_b(w, d, dma_ring_base<F, K>())
-                         : crcdev::raw_dword(w, d, dma_ring_base<F, K>());
+      cacc[q] ^= crcdev::raw_dword(w, d, dma_ring_base<F, K>());
     } else if (static_cast<uint32_t>(q) < p.nrows) {
       crc_store(cpart + q, crcdev::wave_xor(crcdev::lane_map(
                                cacc[q], dma_ring_base<F, K>() + offsetof(CrcLaneTables, lane), lane4)));
@@ -1266,12 +1303,29 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
         }
         if constexpr (DATA) {
           buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x0 + (wave * SW + c) * 1024, x);
-          if (crc)
-            crc_store(p.crc_part_data + (static_cast<uint64_t>(o) * chunks + x0 / 1024 + wave * SW + c) * K + j,
-                      crcdev::chunk_crc(x, dma_ring_base<F, K>(), lane4));
+          uint32_t* dpart = p.crc_part_data + (static_cast<uint64_t>(o) * chunks + x0 / 1024 + wave * SW + c) * K;
+          if constexpr (kMf4 && SW == 1) {
+            // the data chunk's CRC on the matrix cores too: its 8 planes into
+            // an accumulator of its own, the lookups kept per lane, one wave
+            // XOR per 4 inputs (lanes 0..3 store their CRCs)
+            if (crc) {
+              crcdev::mfma_v16i dacc = {};
+#pragma unroll
+              for (int d = 0; d < 8; ++d) dacc = crcdev::mfma_plane(x, d, mb[d], d == 0 ? crcdev::mfma_v16i{} : dacc);
+              dfin[j % 4] = crcdev::mfma_lanes(dacc, dma_ring_base<F, K>() + offsetof(CrcLaneTables, mst), lane4);
+              if (j % 4 == 3 || j == K - 1) {
+                const int n = j % 4 + 1;
+                const uint32_t t = crcdev::wave_xor4(dfin[0], n > 1 ? dfin[1] : 0u, n > 2 ? dfin[2] : 0u,
+                                                     n > 3 ? dfin[3] : 0u, lane_id());
+                if (lane_id() < static_cast<uint32_t>(n)) dpart[j + 1 - n + lane_id()] = t;
+              }
+            }
+          } else if (crc) {
+            crc_store(dpart + j, crcdev::chunk_crc(x, dma_ring_base<F, K>(), lane4));
+          }
         }
       }
-      if constexpr (SW == 1 && (CV == 0 || CV == 3)) {
+      if constexpr (SW == 1 && (CV == 0 || CV == 4 || CV == 6)) {
         if (cpend) {  // the previous item's CRC steps [kCrcSteps j / K, kCrcSteps (j + 1) / K)
 #pragma unroll
           for (int u = j * kCrcSteps / K; u < (j + 1) * kCrcSteps / K; ++u) crc_step(u);
@@ -1288,7 +1342,7 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
         buf_st(parity_row<NR>(p, o, q, par), lane16, soff + q * p.frag_stride, F::row(s[c], q));
       if (crc) {
         uint32_t* part = p.crc_part + (static_cast<uint64_t>(o) * chunks + x0 / 1024 + wave * SW + c) * p.m + p.row0;
-        if constexpr (SW == 1 && (CV == 0 || CV == 3)) {  // taken during the next item (or after the last)
+        if constexpr (SW == 1 && (CV == 0 || CV == 4 || CV == 6)) {  // taken during the next item (or after the last)
 #pragma unroll
           for (int q = 0; q < NR; ++q) {
             crow[q] = F::row(s[c], q);
@@ -1306,7 +1360,7 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
       F::zero(s[c]);
     }
   }
-  if constexpr (SW == 1 && (CV == 0 || CV == 3)) {
+  if constexpr (SW == 1 && (CV == 0 || CV == 4 || CV == 6)) {
     if (cpend) {  // the block's last item
 #pragma unroll
       for (int u = 0; u < kCrcSteps; ++u) crc_step(u);
@@ -2217,7 +2271,7 @@ hipError_t encode_crc_finish(const EncodeParams& p, bool data, uint32_t chunks, 
 // batches keep the stream kernel's 4 KiB items).
 template <class F, int K, int NR, int R, bool NT, int L = 4, int SW = 1, int W = 8,
           bool DATA = false, bool NOCOMP = false, bool CONTIG = false, int RUNS = 0, int COMB = 0,
-          int CV = 0>
+          int CV = 6>
 hipError_t launch_encode_dma(EncodeParams p, hipStream_t stream, uint32_t* chunks = nullptr,
                              bool xcd = true) {
   set_tiles(p, last_room(p.bs, p.obj_len, K), 1024u * W * SW / kTile);
@@ -2360,13 +2414,21 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
   bool done = false;
   if constexpr (kAB && K == 10 && NR == 4) {
     // A/B: the inline CRC's forms (CV, see encode_dma_kernel) and a 4-slot ring
+    // (ECAMD_CRC_V=10: the round-5 lookup form, CV 0; ECAMD_ENC_CV0=1: the
+    // plain and full-stripe encodes built with CV 0, i.e. without the
+    // matrix-core CRC's registers)
     const int cv = ab_knob("ECAMD_CRC_V", 0), cr = ab_knob("ECAMD_CRC_R", 3);
+    if (!crc && ab_knob("ECAMD_ENC_CV0", 0))
+      return data ? launch_encode_dma<F, K, NR, 4, true, 4, 1, 8, true, false, false, 0, 0, 0>(p, stream, &chunks, false)
+                  : launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 0>(p, stream, &chunks);
     if (crc && !data && (cv != 0 || cr != 3)) {
-      if (cv == 1 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 1>(p, stream, &chunks);
+      if (cv == 10 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 0>(p, stream, &chunks);
+      else if (cv == 1 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 1>(p, stream, &chunks);
       else if (cv == 2 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 2>(p, stream, &chunks);
-      else if (cv == 0 && cr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 12>(p, stream, &chunks);
+      else if (cv == 10 && cr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 12, false, false, false, 0, 0, 0>(p, stream, &chunks);
       else if (cv == 1 && cr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 12, false, false, false, 0, 0, 1>(p, stream, &chunks);
-      else if (cv == 3 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 3>(p, stream, &chunks);
+      else if (cv == 4 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 4>(p, stream, &chunks);
+      else if (cv == 4 && cr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 12, false, false, false, 0, 0, 4>(p, stream, &chunks);
       else return hipErrorInvalidValue;
       if (e != hipSuccess) return e;
       return encode_crc_finish<K>(p, data, chunks, stream);

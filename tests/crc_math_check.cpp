@@ -46,6 +46,36 @@ static uint32_t chunk_crc(const CrcLaneTables& L, const uint8_t* c) {
   return a;
 }
 
+// the matrix-core form (crc_device.hpp mfma_plane / mfma_finish), with the
+// operand layout of v_mfma_i32_32x32x32_i8 (tools/mfma_probe.hip checks it
+// on the GPU): row r of A = lanes r and r + 32, B's lane n + 32 g holds
+// column n of K block g, accumulator j of lane l = C[8 (j / 4) + 4 (l / 32) +
+// j % 4][l % 32]; plane b keeps the bits at and above b (those above land
+// on multiples of 256).  Every sum must have bits 0..6 clear (*bad counts those).
+static uint32_t mfma_chunk_crc(const CrcLaneTables& L, const uint8_t* c, int* bad) {
+  int32_t C[32][32] = {};
+  for (int b = 0; b < 8; ++b)
+    for (int r = 0; r < 32; ++r)
+      for (int n = 0; n < 32; ++n)
+        for (int g = 0; g < 2; ++g)
+          for (int e = 0; e < 16; ++e) {
+            const int8_t a = static_cast<int8_t>(c[16 * (r + 32 * g) + e] & (0xFFu << b));
+            C[r][n] += int32_t(a) * int32_t(L.mfb[b][n + 32 * g][e]);
+          }
+  uint32_t acc = 0;
+  for (int l = 0; l < 64; ++l)
+    for (int q = 0; q < 4; ++q) {
+      uint32_t v = 0;
+      for (int i = 0; i < 4; ++i) {
+        const int32_t x = C[8 * q + 4 * (l / 32) + i][l % 32];
+        *bad += (x & 0x7F) != 0;
+        v |= ((static_cast<uint32_t>(x) >> 7) & 1u) << i;
+      }
+      acc ^= L.mst[q][v][l];
+    }
+  return acc;
+}
+
 static uint32_t shift_chunks(const CrcFinishTables& F, uint32_t r, uint32_t d) {
   for (int i = 0; d; ++i, d >>= 1)
     if (d & 1) r = zmap(F.pow[i], r);
@@ -170,6 +200,21 @@ int main() {
       if ((m0 ^ zmap(F->meta, want)) != m1) {
         ++failures;
         std::printf("FAIL meta legacy=%d bs=%u\n", legacy, bs);
+      }
+    }
+  }
+  // the matrix-core form against the lookup form, random and extreme chunks
+  for (int legacy = 0; legacy < 2; ++legacy) {
+    build_crc_lane_tables(legacy != 0, L);
+    for (int t = 0; t < 40; ++t) {
+      uint8_t c[1024];
+      for (auto& b : c) b = t == 0 ? 0xFF : t == 1 ? 0x80 : t == 2 ? 0 : static_cast<uint8_t>(rng());
+      int bad = 0;
+      ++checks;
+      const uint32_t got = mfma_chunk_crc(*L, c, &bad), want = chunk_crc(*L, c);
+      if (got != want || bad) {
+        ++failures;
+        std::printf("FAIL mfma legacy=%d t=%d got %08x want %08x (low bits set %d)\n", legacy, t, got, want, bad);
       }
     }
   }
