@@ -1233,7 +1233,6 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   constexpr int kCrcSteps = kPerRow * NR + (kMf4 ? 1 : 0);
   static_assert(!kMf4 || NR <= 4, "one joint wave XOR");
   uint32_t cfin[kMf4 ? 4 : 1] = {};
-  uint32_t dfin[kMf4 && DATA ? 4 : 1] = {};
   uint4 crow[NR];
   uint32_t cacc[NR];
   uint32_t* cpart = p.crc_part;
@@ -1243,6 +1242,28 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
   if constexpr (kMf) {
     if (crc) crcdev::mfma_load_b(p.crc_lanes, lane_id(), mb);
   }
+  // full stripe: the data chunks' CRCs (input c of an item, its payload
+  // xprev, CRCs stored at base[c]): 8 planes into an accumulator of their
+  // own, the lookups kept per lane, one wave XOR per 4 inputs (lanes 0..3
+  // store the CRCs)
+  uint32_t dfin[kMf4 && DATA ? 4 : 1] = {};
+  uint4 xprev = {};
+  uint32_t* dprev = nullptr;
+  bool dpend = false;
+  auto data_crc = [&](int c, uint32_t* base) {
+    if constexpr (kMf4 && DATA) {
+      crcdev::mfma_v16i dacc = {};
+#pragma unroll
+      for (int d = 0; d < 8; ++d) dacc = crcdev::mfma_plane(xprev, d, mb[d], d == 0 ? crcdev::mfma_v16i{} : dacc);
+      dfin[c % 4] = crcdev::mfma_lanes(dacc, dma_ring_base<F, K>() + offsetof(CrcLaneTables, mst), lane4);
+      if (c % 4 == 3 || c == K - 1) {
+        const int n = c % 4 + 1;
+        const uint32_t t = crcdev::wave_xor4(dfin[0], n > 1 ? dfin[1] : 0u, n > 2 ? dfin[2] : 0u,
+                                             n > 3 ? dfin[3] : 0u, lane_id());
+        if (lane_id() < static_cast<uint32_t>(n)) base[c + 1 - n + lane_id()] = t;
+      }
+    }
+  };
   auto crc_step = [&](int u) {
     if constexpr (kMf4) {
       if (u == kPerRow * NR) {
@@ -1305,19 +1326,17 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
           buf_st(dat, lane16, j * p.frag_stride + kHeaderBytes + x0 + (wave * SW + c) * 1024, x);
           uint32_t* dpart = p.crc_part_data + (static_cast<uint64_t>(o) * chunks + x0 / 1024 + wave * SW + c) * K;
           if constexpr (kMf4 && SW == 1) {
-            // the data chunk's CRC on the matrix cores too: its 8 planes into
-            // an accumulator of its own, the lookups kept per lane, one wave
-            // XOR per 4 inputs (lanes 0..3 store their CRCs)
+            // the data chunk's CRC on the matrix cores too, one slot later
+            // (data_crc: input j - 1 now, the item's last input in the next
+            // item's first slot), so its MFMA chain does not wait on this
+            // slot's LDS read
             if (crc) {
-              crcdev::mfma_v16i dacc = {};
-#pragma unroll
-              for (int d = 0; d < 8; ++d) dacc = crcdev::mfma_plane(x, d, mb[d], d == 0 ? crcdev::mfma_v16i{} : dacc);
-              dfin[j % 4] = crcdev::mfma_lanes(dacc, dma_ring_base<F, K>() + offsetof(CrcLaneTables, mst), lane4);
-              if (j % 4 == 3 || j == K - 1) {
-                const int n = j % 4 + 1;
-                const uint32_t t = crcdev::wave_xor4(dfin[0], n > 1 ? dfin[1] : 0u, n > 2 ? dfin[2] : 0u,
-                                                     n > 3 ? dfin[3] : 0u, lane_id());
-                if (lane_id() < static_cast<uint32_t>(n)) dpart[j + 1 - n + lane_id()] = t;
+              if (j > 0) data_crc(j - 1, dpart);
+              else if (dpend) data_crc(K - 1, dprev);
+              xprev = x;
+              if (j == K - 1) {
+                dprev = dpart;
+                dpend = true;
               }
             }
           } else if (crc) {
@@ -1359,6 +1378,9 @@ __global__ void __launch_bounds__(W * 64) encode_dma_kernel(EncodeParams p) {
       }
       F::zero(s[c]);
     }
+  }
+  if constexpr (kMf4 && DATA && SW == 1) {
+    if (crc && dpend) data_crc(K - 1, dprev);  // the block's last data chunk
   }
   if constexpr (SW == 1 && (CV == 0 || CV == 4 || CV == 6)) {
     if (cpend) {  // the block's last item
@@ -2421,6 +2443,11 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
     if (!crc && ab_knob("ECAMD_ENC_CV0", 0))
       return data ? launch_encode_dma<F, K, NR, 4, true, 4, 1, 8, true, false, false, 0, 0, 0>(p, stream, &chunks, false)
                   : launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 0>(p, stream, &chunks);
+    if (crc && data && cv == 10) {  // the full stripe's CRCs by lookups (CV 0)
+      e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 8, true, false, false, 0, 0, 0>(p, stream, &chunks, false);
+      if (e != hipSuccess) return e;
+      return encode_crc_finish<K>(p, data, chunks, stream);
+    }
     if (crc && !data && (cv != 0 || cr != 3)) {
       if (cv == 10 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 0>(p, stream, &chunks);
       else if (cv == 1 && cr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, false, false, false, 0, 0, 1>(p, stream, &chunks);
@@ -2450,14 +2477,15 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
       if (static_cast<uint64_t>(K) * p.bs + 65536u > 0xFFFFFFFFull) return hipErrorInvalidValue;
       if constexpr (kAB && K == 10 && NR == 4) {
         const int dw = ab_knob("ECAMD_ENC_DATA_W", 8), dr = ab_knob("ECAMD_ENC_DATA_R", 4);
-        if (data && !crc && (dw != 8 || dr != 4)) {
+        if (data && (dw != 8 || dr != 4)) {
           if (dw == 16 && dr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 16, true>(p, stream, &chunks);
           else if (dw == 12 && dr == 4) e = launch_encode_dma<F, K, NR, 4, true, 4, 1, 12, true>(p, stream, &chunks);
           else if (dw == 12 && dr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream, &chunks);
           else if (dw == 8 && dr == 3) e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 8, true>(p, stream, &chunks);
           else if (dw == 8 && dr == 5) e = launch_encode_dma<F, K, NR, 5, true, 4, 1, 8, true>(p, stream, &chunks);
           else return hipErrorInvalidValue;
-          return e;
+          if (e != hipSuccess || !crc) return e;
+          return encode_crc_finish<K>(p, data, chunks, stream);
         }
       }
       // The full stripe (data fragments stored from the ring too) at W = 8,
@@ -2468,7 +2496,18 @@ hipError_t launch_encode_k(EncodeParams p, hipStream_t stream) {
       // grid-stride without the XCD split, 448.5 against 457.3 (r06j).  The
       // plain parity encode stays at W = 12, R = 3, XCD split: at W = 8 its
       // two waves per SIMD cannot hide the lookups (308.0 us against 271.3
-      // at R = 4, 284.8 at R = 5; r06i_ab_alt.txt).
+      // at R = 4, 284.8 at R = 5; r06i_ab_alt.txt).  The full stripe with
+      // the inline CRC (every chunk's CRC on the matrix cores: 14 per item
+      // and wave) runs at W = 12, R = 3 like the parity encode: 587.5 us
+      // against 641.0 at W = 8, R = 4 (637.0 at 16 / 3; r06z_ab_full_crc.txt).
+      // (Four-row GF(2^16) passes only -- m = 3, 4 and the first pass of
+      // larger m: the library's size.)
+      if constexpr (std::is_same_v<F, Gf16<2>> && NR == 4) {
+        if (data && crc) {
+          e = launch_encode_dma<F, K, NR, 3, true, 4, 1, 12, true>(p, stream, &chunks);
+          return e != hipSuccess ? e : encode_crc_finish<K>(p, data, chunks, stream);
+        }
+      }
       e = data ? launch_encode_dma<F, K, NR, 4, true, 4, 1, 8, true>(p, stream, &chunks, false)
                : launch_encode_dma<F, K, NR, 3, true, 4, 1, 12>(p, stream, &chunks);
       done = true;
