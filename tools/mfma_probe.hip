@@ -18,6 +18,12 @@ __global__ void probe(const v4i* a, const v4i* b, v16i* c) {
   const int l = threadIdx.x;
   c[l] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[l], b[l], v16i{}, 0, 0, 0);
 }
+// v_mfma_i32_16x16x64_i8 (the A/B 16x16x64 CRC form): A lane l -> row l % 16,
+// K block l / 16; accumulator j -> C[4 (l / 16) + j][l % 16].
+__global__ void probe16(const v4i* a, const v4i* b, v4i* c) {
+  const int l = threadIdx.x;
+  c[l] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[l], b[l], v4i{}, 0, 0, 0);
+}
 
 static int k_of(int order, int l, int e) {
   return order == 0 ? 16 * (l / 32) + e : 8 * (l / 32) + (e % 8) + 16 * (e / 8);
@@ -59,5 +65,23 @@ int main() {
     if (bad == 0 && matched < 0) matched = order;
   }
   printf(matched == 0 ? "layout as the CRC tables assume\n" : matched == 1 ? "C layout ok, K in halves (same for A and B: the CRC tables hold)\n" : "C LAYOUT DIFFERS\n");
-  return matched < 0 ? 1 : 0;
+  // 16x16x64: K block of 16 per lane group of 16 (order within a block is
+  // the same for A and B either way, as above)
+  int32_t hc16[64][4];
+  void* dc16;
+  if (hipMalloc(&dc16, sizeof hc16)) return 2;
+  probe16<<<1, 64>>>(static_cast<const v4i*>(da), static_cast<const v4i*>(db), static_cast<v4i*>(dc16));
+  if (hipDeviceSynchronize() != hipSuccess) return 3;
+  hipMemcpy(hc16, dc16, sizeof hc16, hipMemcpyDeviceToHost);
+  int bad16 = 0;
+  for (int l = 0; l < 64; ++l)
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * (l / 16) + j, n = l % 16;
+      int want = 0;
+      for (int g = 0; g < 4; ++g)
+        for (int e = 0; e < 16; ++e) want += ha[r + 16 * g][e] * hb[n + 16 * g][e];
+      bad16 += want != hc16[l][j];
+    }
+  printf("16x16x64: %d of 256 accumulators differ from the assumed layout\n", bad16);
+  return (matched < 0 || bad16) ? 1 : 0;
 }
