@@ -50,6 +50,7 @@ import json
 import os
 import subprocess
 import sys
+import statistics
 import time
 
 import numpy as np
@@ -104,6 +105,8 @@ def parse(argv=None):
                     help="decode steps whose erasure masks are new every step (drawn from "
                          "the seed outside the clock, handed over inside it): timed apart "
                          "from the headline step, which replays one batch of masks")
+    ap.add_argument("--crc-steps", type=int, default=10,
+                    help="launches per run of the inline_crc32 encode leg (0: skip it)")
     ap.add_argument("--full-stripe-steps", type=int, default=10,
                     help="launches of the full-stripe encode (k data + m parity fragments, "
                          "headers included: liberasurecode_encode's output) timed after the "
@@ -859,6 +862,49 @@ def fresh_decode(args, codec, stripes, objs, out, stream, B, rank):
                                       "every step's objects compared with the originals"}, ok
 
 
+def crc_encode_leg(args, codec, objs, n, k, m, bs, B, stream):
+    """Per-launch time of the parity encode with and without inline_crc32
+    (CRC kernels + finishing pass), same buffers, back to back."""
+    import zlib
+    import torch
+    from pyeclib_amd import batch
+    crc_codec = batch.BatchCodec(k, m, ec_type=args.ec_type, inline_crc32=True)
+    dev = objs.device
+    st_plain = batch.stripe_buffer(B, k, m, bs, device=dev)
+    st_crc = batch.stripe_buffer(B, k, m, bs, device=dev)
+    steps = args.crc_steps
+    ms = {}
+    for name, c, st in (("plain", codec, st_plain), ("crc", crc_codec, st_crc), ("plain2", codec, st_plain),
+                        ("crc2", crc_codec, st_crc)):
+        c.encode(objs, n, parity=st[:, k:])
+        torch.cuda.synchronize()
+        # an event pair around every call: the device time of its launches
+        # (the CRC encode's finishing pass included), not the host's pace
+        mk = HipEvent if args.events == "nofence" else (lambda: torch.cuda.Event(enable_timing=True))
+        ev = [(mk(), mk()) for _ in range(steps)]
+        for a, b in ev:
+            a.record(stream)
+            c.encode(objs, n, parity=st[:, k:])
+            b.record(stream)
+        torch.cuda.synchronize()
+        ms[name] = statistics.median([a.elapsed_time(b) for a, b in ev])
+    # payloads equal, and chksum[0] (header bytes 21..24) = crc32 of the payload
+    ok = bool(torch.equal(st_plain[:, k:, 80:80 + bs], st_crc[:, k:, 80:80 + bs]))
+    for o in sorted({0, B // 3, B // 2, B - 1}):
+        for q in range(m):
+            frag = st_crc[o, k + q, :80 + bs].cpu().numpy().tobytes()
+            ok = ok and int.from_bytes(frag[21:25], "little") == zlib.crc32(frag[80:80 + bs])
+    plain, crc = min(ms["plain"], ms["plain2"]), min(ms["crc"], ms["crc2"])
+    del st_plain, st_crc, crc_codec
+    return {"ms": round(crc, 4), "plain_ms": round(plain, 4), "vs_plain": round(crc / plain, 3),
+            "launches": 2 * steps, "verified_sample": ok,
+            "note": "parity-only encode with chksum_type inline_crc32 (chunk CRCs on the matrix cores "
+                    "+ the finishing pass) against the plain parity encode, on this box: an event pair "
+                    "(the headline's kind) around every call (device time), the median of `launches`/2 "
+                    "calls, the faster of two runs each; "
+                    "headers of 4 objects checked against zlib.crc32"}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -1105,6 +1151,17 @@ def main():
             "launches": args.full_stripe_steps,
             "note": "k data + m parity fragments with headers per object in one launch, back "
                     "to back; these stripes are the ones the oracle check below compares"}
+
+    # ---- inline_crc32 encode beside the plain one (round 6: the chunk CRCs on
+    # the matrix cores): the same batch, parity only,
+    # both back to back on this box, so the ratio is the CRC's cost; a
+    # sample of headers checked against zlib's crc32 of their payloads.  An
+    # auxiliary leg: recorded, never fatal to the headline ----
+    if args.crc_steps > 0 and not args.inline_crc32 and args.ec_type in ("amd_rs_vand", "liberasurecode_rs_vand"):
+        try:
+            result["encode_inline_crc32"] = crc_encode_leg(args, codec, objs, n, k, m, bs, B, stream)
+        except Exception as exc:  # noqa: BLE001
+            result["encode_inline_crc32"] = {"error": repr(exc)[:300]}
 
     # ---- verification of the timed batch (every object), and the CPU baseline ----
     bad = []

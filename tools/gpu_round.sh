@@ -85,16 +85,16 @@ for s in $STEPS; do
     # so the last 20 dispatches of each kernel are the timed steps), summarised
     # into kernel_stats.json for bench.py's roofline (frac_rocprof)
     (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run \
-      -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-verify --no-host \
+      -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-verify --no-host --crc-steps 0 \
       --fresh-steps 0 --full-stripe-steps 0 > $O/prof_bench.json 2> $O/prof.err)
     cat $O/prof_bench.json
     python3 $R/tools/kernel_stats_summary.py $O/prof $O/kernel_stats.json --steps 20
     find $O/prof -name '*kernel_stats.csv' -exec cp {} $O/kernel_stats.csv \; ;;
   pmc)
     (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run \
-      -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host > $O/pmc_fetch.log 2>&1)
+      -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host --crc-steps 0 > $O/pmc_fetch.log 2>&1)
     (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run \
-      -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host > $O/pmc_write.log 2>&1)
+      -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host --crc-steps 0 > $O/pmc_write.log 2>&1)
     python3 $R/tools/pmc_summary.py $O/pmc_fetch $O/pmc_write $O/pmc_summary.json ;;
   list)
     (cd /tmp && timeout -k 10 120 rocprofv3 -L > $O/counters.txt 2>&1) || true
@@ -102,7 +102,7 @@ for s in $STEPS; do
   sq)
     for f in ${SQ_FILES:-pmc1 pmc2 pmc3}; do
       (cd /tmp && timeout -s KILL 150 rocprofv3 -i $R/tools/$f.txt --output-format csv -d $O/sq_$f -o run \
-        -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host ${SQ_ARGS:-} > $O/sq_$f.log 2>&1)
+        -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-host --crc-steps 0 ${SQ_ARGS:-} > $O/sq_$f.log 2>&1)
     done
     python3 $R/tools/pmc_table.py $(for f in ${SQ_FILES:-pmc1 pmc2 pmc3}; do echo $O/sq_$f; done) > $O/sq_table.txt 2>&1 || true
     cat $O/sq_table.txt ;;
